@@ -1,0 +1,245 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X acoustic-scoring path (BASELINE.json configs[2]/[3]).
+
+Workload (config C3 of SURVEY.md 8): the full am.cc pipeline -- fbank ->
+online CMVN -> TDNN-S nnet (Splice/Linear/ReLU/BatchNorm x6, Linear 1024->3456,
+LogSoftmax) -> minus log prior -- in fp32, one step = one packed frame batch of
+at most 4096 rows = four 10 s synthetic 16 kHz utterances (4 x 998 = 3992
+output frames, 4 x 1018 = 4072 packed rows).  PCM for a pool of utterances is
+resident in HBM before timing; weights are random-init TDNN-S in the
+reference's NN02 format (no model ships with the reference).
+
+One process per GPU (torchrun); each rank scores its own utterances (weak
+scaling); for N > 1 every rank's log-likelihood batch is gathered to rank 0
+with RCCL over xGMI (torch.distributed "nccl"), overlapped with the next step.
+
+Prints ONE JSON line (rank 0).  See DESIGN.md "Measurement" for every field.
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FLOPS_PER_FRAME = 2 * (200 * 1024 + 4 * 3072 * 1024 + 1024 * 1024 + 1024 * 3456)  # 34,750,464
+# FLOPs per output frame of the GEMMs timed as CE_GPU_PROF_GEMM (all but layer 1)
+FLOPS_PER_FRAME_FAST = FLOPS_PER_FRAME - 2 * 200 * 1024
+MFMA_F32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: dense fp32 MFMA (= vector) peak
+HBM_PEAK_GBS = 8000.0
+METRIC = "acoustic frames/sec (fbank->nnet posteriors), 16kHz, 1/2/4/8 GPU"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--utts-per-step", type=int, default=4)
+    ap.add_argument("--pool", type=int, default=32, help="distinct utterances resident per rank")
+    ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--model", default="tdnn-s")
+    ap.add_argument("--no-cmvn", action="store_true")
+    ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--cpu-utts", type=int, default=32, help="utterances in the CPU baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true", help="skip the HIP-event kernel timing")
+    return ap.parse_args()
+
+
+def cpu_baseline(conf, n_utts, seconds, threads):
+    """Oracle restatement ('port') of fbank -> CMVN -> nnet -> -log prior on the
+    host cores: one utterance per worker thread, single-threaded OpenBLAS sgemm
+    (numpy) inside each worker, like the reference's cblas_sgemm path."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from catears_amd import formats, synth
+    from oracle import pyoracle
+    try:
+        from threadpoolctl import threadpool_limits
+    except ImportError:  # pragma: no cover
+        threadpool_limits = None
+    am = formats.read_am(conf)
+    gstats = synth.cmvn_stats_synthetic()
+    n = int(16000 * seconds)
+    waves = [synth.pcm(900000 + i, n) for i in range(n_utts)]
+
+    def one(w):
+        fb = pyoracle.Fbank()
+        f = pyoracle.cmvn(gstats, fb.compute(w))
+        return pyoracle.am_whole(am, f, gemm=lambda a, b: a @ b).shape[0]
+
+    ctxm = threadpool_limits(limits=1) if threadpool_limits else None
+    try:
+        one(waves[0][:16000])  # warm up
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(threads) as ex:
+            frames = sum(ex.map(one, waves))
+        dt = time.perf_counter() - t0
+    finally:
+        if ctxm is not None:
+            ctxm.__exit__(None, None, None)
+    return frames / dt, frames, dt
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from catears_amd import gpu, synth
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    # synthetic TDNN-S model, written once per node
+    mdir = os.path.join(tempfile.gettempdir(), f"catears_bench_{os.getuid()}")
+    if local == 0:
+        synth.write_model(mdir, args.model)
+    if world > 1:
+        dist.barrier()
+    conf = synth.write_model(mdir, args.model)  # no-op once written
+
+    stream = torch.cuda.current_stream()
+    ctx = gpu.Context(local, stream)
+    model = gpu.Model(ctx, conf)
+    n_samp = int(16000 * args.seconds)
+    U = args.utts_per_step
+    plan = gpu.Plan(ctx, [n_samp] * U, model, max_rows=4096)
+    frames_per_step = plan.total_frames
+    assert plan.n_chunks == 1, "a step must be one frame batch"
+
+    # resident PCM pool (distinct utterances per rank)
+    pool = max(args.pool, U)
+    pcm = torch.from_numpy(np.stack([synth.pcm(rank * 100003 + i, n_samp) for i in range(pool)])).cuda()
+    gstats = None if args.no_cmvn else torch.from_numpy(synth.cmvn_stats_synthetic()).cuda()
+    ws = torch.empty(2 * frames_per_step * 40 + 1, dtype=torch.float32, device="cuda")
+    nbuf = 3
+    outs = [torch.empty((frames_per_step, model.num_pdfs), dtype=torch.float32, device="cuda")
+            for _ in range(nbuf)]
+    gather = world > 1 and not args.no_gather
+    recv = None
+    if gather and rank == 0:
+        recv = [[torch.empty_like(outs[0]) for _ in range(world)] for _ in range(nbuf)]
+    pending = [None] * nbuf
+    checksum = torch.zeros((), dtype=torch.float64, device="cuda")
+
+    def step(i):
+        slot = i % nbuf
+        if pending[slot] is not None:
+            pending[slot].wait()  # gather from nbuf steps ago has read this buffer
+            pending[slot] = None
+        first = (i * U) % (pool - U + 1)
+        src = pcm[first:first + U].reshape(-1)
+        gpu.score(ctx, model, plan, src, gstats, ws, outs[slot])
+        if gather:
+            pending[slot] = dist.gather(outs[slot], recv[slot] if rank == 0 else None, dst=0,
+                                        async_op=True)
+
+    for i in range(args.warmup):
+        step(i)
+    for w in pending:
+        if w is not None:
+            w.wait()
+    pending = [None] * nbuf
+    torch.cuda.synchronize()
+    if not args.no_profile:
+        ctx.profile(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    for w in pending:
+        if w is not None:
+            w.wait()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    # the outputs are consumed (checksum) so no work can be elided
+    checksum += outs[(args.warmup + args.steps - 1) % nbuf].double().sum()
+    finite = bool(torch.isfinite(outs[0]).all().item())
+
+    prof = {}
+    if not args.no_profile:
+        ctx.profile(False)
+        for name, cls in (("gemm", ctx.PROF_GEMM), ("gemm_gather", ctx.PROF_GEMM_GATHER),
+                          ("fbank", ctx.PROF_FBANK), ("cmvn", ctx.PROF_CMVN), ("finalize", ctx.PROF_FINALIZE)):
+            prof[name] = ctx.profile_read(cls)
+
+    total_frames = frames_per_step * args.steps * world
+    value = total_frames / elapsed
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    roofline = None
+    stages = {}
+    if prof:
+        ms, n = prof["gemm"]
+        if n:
+            flops_per_launch = frames_per_step * FLOPS_PER_FRAME_FAST / (n / args.steps)
+            avg_ms = ms / n
+            achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
+            roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": MFMA_F32_PEAK_TFLOPS,
+                        "unit": "TFLOP/s", "frac": round(achieved / MFMA_F32_PEAK_TFLOPS, 4),
+                        "traffic": None, "kernel": "gemm_f32_kernel<true,false> (TDNN layers 2-7)",
+                        "launches": n, "avg_launch_ms": round(avg_ms, 4),
+                        "flops_per_launch": flops_per_launch}
+        for name, (ms, n) in prof.items():
+            if n:
+                stages[name] = {"launches": n, "avg_ms": round(ms / n, 4),
+                                "share_of_step": round(ms / (elapsed * 1e3), 4)}
+        if "fbank" in stages:
+            fb_bytes = 4 * U * n_samp + 4 * 40 * frames_per_step  # PCM read once + features written
+            stages["fbank"]["hbm_GBs"] = round(fb_bytes / (stages["fbank"]["avg_ms"] * 1e-3) / 1e9, 1)
+            stages["fbank"]["hbm_frac"] = round(stages["fbank"]["hbm_GBs"] / HBM_PEAK_GBS, 4)
+
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        threads = min(16, os.cpu_count() or 1)
+        v, fr, dt = cpu_baseline(conf, args.cpu_utts, args.seconds, threads)
+        cpu = {"value": round(v, 1), "unit": "frames/s", "cores": threads, "kind": "port",
+               "sample": f"{args.cpu_utts} x {args.seconds:g} s utterances ({fr} frames, {dt:.1f} s wall): "
+                         f"oracle fbank+CMVN (C) + TDNN-S with single-threaded OpenBLAS sgemm per worker"}
+
+    line = {
+        "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (seeded 16 kHz PCM, random-init TDNN-S in NN02 format)",
+        "config": {"workload": "C3 full pipeline fbank->CMVN->TDNN-S->loglik, frame batch <= 4096 rows "
+                               f"({U} x {args.seconds:g} s utterances/step/GPU)" +
+                               ("" if not gather else "; C4 RCCL gather of log-likelihoods to rank 0"),
+                   "frames_per_step_per_gpu": frames_per_step, "packed_rows": plan.max_chunk_rows,
+                   "cmvn": not args.no_cmvn, "parallelism": f"utterance shard x{world}",
+                   "gather": gather},
+        "roofline": roofline, "cpu_baseline": cpu, "stages": stages,
+        "end_to_end_mfma_frac": round(value / world * FLOPS_PER_FRAME / 1e12 / MFMA_F32_PEAK_TFLOPS, 4),
+        "checksum": float(checksum.item()), "finite": finite,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

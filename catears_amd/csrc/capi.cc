@@ -1,0 +1,837 @@
+// capi.cc -- extern "C" entry points of libcatears_hip (include/catears_gpu.h):
+// errors, contexts, model loading (NN02 / MAT0 / VEC0 / key=value config),
+// batch planning, and the host-side sequencing of the kernels.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cctype>
+#include <fstream>
+#include <map>
+#include <memory>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "internal.h"
+
+namespace catears {
+
+// ---------------------------------------------------------------- errors --
+
+static thread_local std::string g_last_error;
+
+int fail(int code, const std::string &msg) {
+  g_last_error = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char *what) {
+  return fail(CE_GPU_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+static std::string fmt(const char *f, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, f);
+  vsnprintf(buf, sizeof(buf), f, ap);
+  va_end(ap);
+  return buf;
+}
+
+// ---------------------------------------------------------------- DevBuf --
+
+int DevBuf::alloc(size_t n) {
+  release();
+  if (n == 0) return CE_GPU_OK;
+  hipError_t e = hipMalloc(&ptr, n);
+  if (e != hipSuccess) {
+    ptr = nullptr;
+    (void)hipGetLastError();
+    return fail(CE_GPU_ENOMEM, fmt("hipMalloc(%zu) failed: %s", n, hipGetErrorString(e)));
+  }
+  bytes = n;
+  return CE_GPU_OK;
+}
+
+int DevBuf::upload(const void *src, size_t n) {
+  CE_TRY(alloc(n));
+  if (n) CE_HIP(hipMemcpy(ptr, src, n, hipMemcpyHostToDevice));
+  return CE_GPU_OK;
+}
+
+void DevBuf::release() {
+  if (ptr) (void)hipFree(ptr);
+  ptr = nullptr;
+  bytes = 0;
+}
+
+// ----------------------------------------------------------- file reading --
+
+// Little-endian binary reader with the reference's error strings
+// (src/util.cc:123-153).
+struct Reader {
+  FILE *f = nullptr;
+  std::string name;
+  ~Reader() {
+    if (f) fclose(f);
+  }
+  int open(const std::string &path) {
+    name = path;
+    f = fopen(path.c_str(), "rb");
+    if (!f) return fail(CE_GPU_EIO, "IOError: Unable to open " + path);
+    return CE_GPU_OK;
+  }
+  int read(void *dst, size_t n) {
+    if (n == 0) return CE_GPU_OK;
+    if (fread(dst, n, 1, f) != 1) return fail(CE_GPU_EIO, "IOError: failed to read: " + name);
+    return CE_GPU_OK;
+  }
+  int i32(int32_t *v) { return read(v, 4); }
+  int tag(const char *expect) {
+    char got[5] = {0};
+    CE_TRY(read(got, 4));
+    if (memcmp(got, expect, 4) != 0)
+      return fail(CE_GPU_ECORRUPT, fmt("Corruption: ReadAndVerifyString: '%s' expected but '%s' found in %s",
+                                       expect, got, name.c_str()));
+    return CE_GPU_OK;
+  }
+  // Vector<Real>::Read (src/vector.cc:267-300), Real of size 4
+  template <typename T>
+  int vec(std::vector<T> *out) {
+    static_assert(sizeof(T) == 4, "VEC0 payloads here are 4-byte");
+    CE_TRY(tag("VEC0"));
+    int32_t section = 0, dim = 0;
+    CE_TRY(i32(&section));
+    CE_TRY(i32(&dim));
+    if (dim < 0 || (int64_t)dim * 4 + 4 != section)
+      return fail(CE_GPU_ECORRUPT, fmt("Corruption: section_size = %d * 4 + 4 expected, but %d found: %s",
+                                       dim, section, name.c_str()));
+    out->resize(dim);
+    return read(out->data(), (size_t)dim * 4);
+  }
+  // Matrix<float>::Read (src/matrix.cc:159-191)
+  int mat(std::vector<float> *out, int *rows, int *cols) {
+    CE_TRY(tag("MAT0"));
+    int32_t section = 0, r = 0, c = 0;
+    CE_TRY(i32(&section));
+    CE_TRY(i32(&r));
+    CE_TRY(i32(&c));
+    if (r < 0 || c < 0) return fail(CE_GPU_ECORRUPT, "Corruption: negative matrix shape in " + name);
+    out->resize((size_t)r * c);
+    std::vector<float> row;
+    for (int i = 0; i < r; ++i) {
+      CE_TRY(vec(&row));
+      if ((int)row.size() != c)
+        return fail(CE_GPU_ECORRUPT,
+                    fmt("Corruption: Matrix::Read: row_read.Dim() == %d expected, but %d found: %s", c,
+                        (int)row.size(), name.c_str()));
+      std::copy(row.begin(), row.end(), out->begin() + (size_t)i * c);
+    }
+    *rows = r;
+    *cols = c;
+    return CE_GPU_OK;
+  }
+};
+
+// Configuration::Read (src/configuration.cc:14-50): key = value, '#' comments,
+// keys case-insensitive, paths relative to the config file's directory.
+struct Config {
+  std::string file;
+  std::map<std::string, std::string> kv;
+  static std::string trim(const std::string &s) {
+    size_t a = 0, b = s.size();
+    while (a < b && isspace((unsigned char)s[a])) ++a;
+    while (b > a && isspace((unsigned char)s[b - 1])) --b;
+    return s.substr(a, b - a);
+  }
+  int read(const std::string &path) {
+    file = path;
+    std::ifstream in(path);
+    if (!in) return fail(CE_GPU_EIO, "IOError: Unable to open " + path);
+    std::string line;
+    while (std::getline(in, line)) {
+      while (!line.empty() && (line.back() == '\r' || line.back() == '\n')) line.pop_back();
+      line = trim(line);
+      if (line.empty() || line[0] == '#') continue;
+      size_t eq = line.find('=');
+      if (eq == std::string::npos || line.find('=', eq + 1) != std::string::npos)
+        return fail(CE_GPU_ECORRUPT, "Corruption: Unexpected line in " + path + ": " + line);
+      std::string k = trim(line.substr(0, eq)), v = trim(line.substr(eq + 1));
+      if (v.empty()) return fail(CE_GPU_ECORRUPT, "Corruption: Value cound not be empty: " + path);
+      std::transform(k.begin(), k.end(), k.begin(), [](unsigned char ch) { return (char)tolower(ch); });
+      kv[k] = v;
+    }
+    return CE_GPU_OK;
+  }
+  int get(const std::string &key, std::string *v) const {
+    auto it = kv.find(key);
+    if (it == kv.end())
+      return fail(CE_GPU_ECORRUPT, "Corruption: Unable to find key '" + key + "' in '" + file + "'");
+    *v = it->second;
+    return CE_GPU_OK;
+  }
+  int path(const std::string &key, std::string *v) const {
+    CE_TRY(get(key, v));
+    if ((*v)[0] == '/') return CE_GPU_OK;
+    size_t slash = file.rfind('/');
+    if (slash != std::string::npos) *v = file.substr(0, slash + 1) + *v;
+    return CE_GPU_OK;
+  }
+  int integer(const std::string &key, int *v) const {
+    std::string s;
+    CE_TRY(get(key, &s));
+    char *end = nullptr;
+    long x = strtol(s.c_str(), &end, 10);
+    if (end == s.c_str()) return fail(CE_GPU_ECORRUPT, "Corruption: not an integer: " + key);
+    *v = (int)x;
+    return CE_GPU_OK;
+  }
+};
+
+// ------------------------------------------------------------ nnet model --
+
+// Layer ids (src/nnet.h:21-30).
+enum LayerId { kLinear = 0, kReLU = 1, kNormalize = 2, kSoftmax = 3, kSplice = 6, kBatchNorm = 7,
+               kLogSoftmax = 8, kNarrow = 9 };
+
+struct RawLayer {
+  int id = -1;
+  std::vector<float> w, b, scale, offset;  // linear: w is in x out
+  int rows = 0, cols = 0;
+  std::vector<int32_t> idx;  // splice
+  int left = 0, right = 0;   // narrow
+};
+
+// Nnet::Read / ReadLayer (src/nnet.cc:221-293)
+static int read_nnet(const std::string &path, std::vector<RawLayer> *layers, int *hl, int *hr) {
+  Reader rd;
+  CE_TRY(rd.open(path));
+  CE_TRY(rd.tag("NN02"));
+  int32_t l = 0, r = 0, n = 0;
+  CE_TRY(rd.i32(&l));
+  CE_TRY(rd.i32(&r));
+  CE_TRY(rd.i32(&n));
+  *hl = l;
+  *hr = r;
+  for (int i = 0; i < n; ++i) {
+    RawLayer L;
+    CE_TRY(rd.tag("LAY0"));
+    int32_t id = 0;
+    CE_TRY(rd.i32(&id));
+    L.id = id;
+    switch (id) {
+      case kLinear:
+        CE_TRY(rd.mat(&L.w, &L.rows, &L.cols));
+        CE_TRY(rd.vec(&L.b));
+        break;
+      case kReLU:
+      case kNormalize:
+      case kSoftmax:
+      case kLogSoftmax:
+        break;
+      case kSplice: {
+        int32_t cnt = 0;
+        CE_TRY(rd.i32(&cnt));
+        if (cnt < 0) return fail(CE_GPU_ECORRUPT, "Corruption: SpliceLayer: unexpected num_indcies");
+        L.idx.resize(cnt);
+        for (int k = 0; k < cnt; ++k) CE_TRY(rd.i32(&L.idx[k]));
+        break;
+      }
+      case kBatchNorm:
+        CE_TRY(rd.vec(&L.scale));
+        CE_TRY(rd.vec(&L.offset));
+        break;
+      case kNarrow:
+        CE_TRY(rd.i32(&L.left));
+        CE_TRY(rd.i32(&L.right));
+        break;
+      default:
+        return fail(CE_GPU_ECORRUPT, fmt("Corruption: read_layer: unexpected layer type: %d (%s)", id,
+                                         path.c_str()));
+    }
+    layers->push_back(std::move(L));
+  }
+  return CE_GPU_OK;
+}
+
+// Turns the layer list into fused device steps.  The reference's converter
+// always emits Splice immediately followed by Narrow(-min(idx,0), max(idx,0))
+// (tool/convert_am.py:272-285); under that shape the output of a chunk does
+// not depend on where the chunk boundaries are, which is what lets the GPU run
+// whole utterances.  Other shapes are rejected with CE_GPU_ENOTSUP.
+static int build_program(const std::vector<RawLayer> &layers, int left, int right, ce_gpu_model *m) {
+  std::vector<int> pending;  // splice offsets waiting for their Linear
+  bool have_pending = false, gemm_open = false;
+  int width = -1, sum_l = 0, sum_r = 0;
+  for (size_t i = 0; i < layers.size(); ++i) {
+    const RawLayer &L = layers[i];
+    switch (L.id) {
+      case kSplice: {
+        if (have_pending) return fail(CE_GPU_ENOTSUP, "two Splice layers without a Linear between them");
+        if (L.idx.empty() || L.idx.size() > 8) return fail(CE_GPU_ENOTSUP, "Splice needs 1..8 indices");
+        int lo = 0, hi = 0;
+        for (int v : L.idx) lo = std::min(lo, v), hi = std::max(hi, v);
+        if (i + 1 >= layers.size() || layers[i + 1].id != kNarrow || layers[i + 1].left != -lo ||
+            layers[i + 1].right != hi)
+          return fail(CE_GPU_ENOTSUP, "Splice must be followed by Narrow(-min(idx,0), max(idx,0))");
+        pending.assign(L.idx.begin(), L.idx.end());
+        have_pending = true;
+        gemm_open = false;
+        ++i;  // the Narrow
+        sum_l += -lo;
+        sum_r += hi;
+        if (!(i + 1 < layers.size() && layers[i + 1].id == kLinear))
+          return fail(CE_GPU_ENOTSUP, "Splice/Narrow must feed a Linear layer");
+        break;
+      }
+      case kNarrow:
+        if (L.left != 0 || L.right != 0) return fail(CE_GPU_ENOTSUP, "Narrow without a preceding Splice");
+        break;
+      case kLinear: {
+        Step st;
+        GemmLayer &g = st.gemm;
+        const int in = L.rows, out = L.cols;
+        if ((int)L.b.size() != out)
+          return fail(CE_GPU_ECORRUPT, "Corruption: Linear bias size does not match W");
+        g.nseg = have_pending ? (int)pending.size() : 1;
+        if (in % g.nseg != 0) return fail(CE_GPU_ECORRUPT, "Corruption: Linear input does not match Splice");
+        g.din = in / g.nseg;
+        for (int s = 0; s < g.nseg; ++s) g.off[s] = have_pending ? pending[s] : 0;
+        if (width >= 0 && g.din != width)
+          return fail(CE_GPU_ECORRUPT, fmt("Corruption: layer %zu expects width %d, got %d", i, g.din, width));
+        if (m->steps.empty()) m->input_dim = g.din;
+        g.k = in;
+        g.kpad = (in + 31) / 32 * 32;
+        g.n = out;
+        std::vector<float> wt((size_t)out * g.kpad, 0.0f);  // transpose to n x kpad
+        for (int k = 0; k < in; ++k)
+          for (int j = 0; j < out; ++j) wt[(size_t)j * g.kpad + k] = L.w[(size_t)k * out + j];
+        CE_TRY(g.wt.upload(wt.data(), wt.size() * 4));
+        CE_TRY(g.bias.upload(L.b.data(), L.b.size() * 4));
+        m->num_params += (int64_t)in * out + out;
+        m->max_width = std::max(m->max_width, out);
+        ++m->num_linear;
+        m->steps.push_back(std::move(st));
+        have_pending = false;
+        gemm_open = true;
+        width = out;
+        break;
+      }
+      case kReLU:
+      case kBatchNorm: {
+        if (width < 0) return fail(CE_GPU_ENOTSUP, "the first layer must be a (spliced) Linear");
+        if (L.id == kBatchNorm && ((int)L.scale.size() != width || (int)L.offset.size() != width))
+          return fail(CE_GPU_ECORRUPT, "Corruption: BatchNorm size does not match its input");
+        GemmLayer &g = m->steps.back().gemm;
+        const bool bn_free = L.id != kBatchNorm || !g.bn_scale.ptr;
+        if (gemm_open && m->steps.back().is_gemm && g.npost < 4 && bn_free) {
+          g.post[g.npost++] = L.id == kReLU ? kPostRelu : kPostBatchNorm;
+          if (L.id == kBatchNorm) {
+            CE_TRY(g.bn_scale.upload(L.scale.data(), width * 4));
+            CE_TRY(g.bn_offset.upload(L.offset.data(), width * 4));
+            m->num_params += 2 * width;
+          }
+        } else {
+          Step st;
+          st.is_gemm = false;
+          st.row.kind = L.id == kReLU ? kRowRelu : kRowBatchNorm;
+          st.row.dim = width;
+          if (L.id == kBatchNorm) {
+            CE_TRY(st.row.scale.upload(L.scale.data(), width * 4));
+            CE_TRY(st.row.offset.upload(L.offset.data(), width * 4));
+          }
+          m->steps.push_back(std::move(st));
+          gemm_open = false;
+        }
+        break;
+      }
+      case kLogSoftmax:
+      case kSoftmax:
+      case kNormalize: {
+        if (width < 0) return fail(CE_GPU_ENOTSUP, "the first layer must be a (spliced) Linear");
+        if (L.id == kLogSoftmax && i + 1 == layers.size()) {
+          m->final_log_softmax = true;
+        } else {
+          Step st;
+          st.is_gemm = false;
+          st.row.kind = L.id == kLogSoftmax ? kRowLogSoftmax : (L.id == kSoftmax ? kRowSoftmax : kRowNormalize);
+          st.row.dim = width;
+          m->steps.push_back(std::move(st));
+        }
+        gemm_open = false;
+        break;
+      }
+      default:
+        return fail(CE_GPU_ECORRUPT, "Corruption: unexpected layer");
+    }
+  }
+  if (m->steps.empty() || !m->steps.front().is_gemm)
+    return fail(CE_GPU_ENOTSUP, "the nnet must start with a (spliced) Linear layer");
+  if (sum_l != left || sum_r != right)
+    return fail(CE_GPU_ECORRUPT, fmt("Corruption: config context (%d, %d) differs from the nnet's (%d, %d)",
+                                     left, right, sum_l, sum_r));
+  m->num_pdfs = width;
+  return CE_GPU_OK;
+}
+
+static int load_model(ce_gpu_ctx *ctx, const std::string &nnet, const std::string &prior, int left,
+                      int right, const std::string &tid2pdf, ce_gpu_model **out) {
+  CE_HIP(hipSetDevice(ctx->device));
+  std::unique_ptr<ce_gpu_model> m(new (std::nothrow) ce_gpu_model());
+  if (!m) return fail(CE_GPU_ENOMEM, "out of host memory");
+  if (left < 0 || right < 0) return fail(CE_GPU_EINVAL, "negative context");
+  m->left = left;
+  m->right = right;
+  std::vector<RawLayer> layers;
+  int hl = 0, hr = 0;
+  CE_TRY(read_nnet(nnet, &layers, &hl, &hr));
+  CE_TRY(build_program(layers, left, right, m.get()));
+  // prior: VEC0, then ApplyLog (src/am.cc:40-44)
+  Reader rd;
+  CE_TRY(rd.open(prior));
+  std::vector<float> pr;
+  CE_TRY(rd.vec(&pr));
+  if ((int)pr.size() != m->num_pdfs)
+    return fail(CE_GPU_ECORRUPT, fmt("Corruption: prior has %d entries, nnet outputs %d", (int)pr.size(),
+                                     m->num_pdfs));
+  for (float &v : pr) v = logf(v);
+  CE_TRY(m->log_prior.upload(pr.data(), pr.size() * 4));
+  if (!tid2pdf.empty()) {
+    Reader rt;
+    CE_TRY(rt.open(tid2pdf));
+    CE_TRY(rt.vec(&m->tid2pdf));
+  }
+  *out = m.release();
+  return CE_GPU_OK;
+}
+
+// ------------------------------------------------------------ workspace --
+
+static int ensure_workspace(ce_gpu_ctx *ctx, size_t floats) {
+  if (ctx->workspace_floats >= floats) return CE_GPU_OK;
+  CE_HIP(hipStreamSynchronize(ctx->stream));  // old buffer may still be in use
+  CE_TRY(ctx->workspace.alloc(floats * sizeof(float)));
+  ctx->workspace_floats = floats;
+  return CE_GPU_OK;
+}
+
+static int ensure_scratch(ce_gpu_ctx *ctx, size_t bytes) {
+  if (ctx->scratch.bytes >= bytes) return CE_GPU_OK;
+  CE_HIP(hipStreamSynchronize(ctx->stream));
+  return ctx->scratch.alloc(bytes);
+}
+
+int fbank_frames_per_block();
+
+static hipEvent_t pool_event(ce_gpu_ctx *ctx) {
+  if (!ctx->event_pool.empty()) {
+    hipEvent_t e = ctx->event_pool.back();
+    ctx->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+ProfScope::ProfScope(ce_gpu_ctx *c, int k) : ctx(c), cls(k) {
+  if (!ctx->profiling) return;
+  hipEvent_t a = pool_event(ctx);
+  b = pool_event(ctx);
+  if (!a || !b) {
+    b = nullptr;
+    return;
+  }
+  (void)hipEventRecord(a, ctx->stream);
+  ctx->timed.push_back({cls, a, b});
+}
+
+ProfScope::~ProfScope() {
+  if (b) (void)hipEventRecord(b, ctx->stream);
+}
+
+}  // namespace catears
+
+using namespace catears;
+
+// =================================================================== ABI ==
+
+extern "C" {
+
+const char *ce_gpu_last_error(void) { return g_last_error.c_str(); }
+
+const char *ce_gpu_version(void) { return "catears-mi355x 0.1 (gfx950)"; }
+
+int ce_gpu_ctx_create(int device, void *stream, ce_gpu_ctx **out) {
+  if (!out) return fail(CE_GPU_EINVAL, "out is NULL");
+  *out = nullptr;
+  int n = 0;
+  CE_HIP(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return fail(CE_GPU_EINVAL, fmt("no HIP device %d (have %d)", device, n));
+  CE_HIP(hipSetDevice(device));
+  std::unique_ptr<ce_gpu_ctx> c(new (std::nothrow) ce_gpu_ctx());
+  if (!c) return fail(CE_GPU_ENOMEM, "out of host memory");
+  c->device = device;
+  c->stream = static_cast<hipStream_t>(stream);
+  build_fbank_tables(&c->host_tables);
+  CE_TRY(c->d_tables.upload(&c->host_tables, sizeof(FbankTables)));
+  *out = c.release();
+  return CE_GPU_OK;
+}
+
+int ce_gpu_ctx_destroy(ce_gpu_ctx *ctx) {
+  if (!ctx) return CE_GPU_OK;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  for (auto &t : ctx->timed) (void)hipEventDestroy(t.a), (void)hipEventDestroy(t.b);
+  for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
+  delete ctx;
+  return CE_GPU_OK;
+}
+
+int ce_gpu_ctx_set_stream(ce_gpu_ctx *ctx, void *stream) {
+  if (!ctx) return fail(CE_GPU_EINVAL, "ctx is NULL");
+  ctx->stream = static_cast<hipStream_t>(stream);
+  return CE_GPU_OK;
+}
+
+int ce_gpu_ctx_synchronize(ce_gpu_ctx *ctx) {
+  if (!ctx) return fail(CE_GPU_EINVAL, "ctx is NULL");
+  CE_HIP(hipStreamSynchronize(ctx->stream));
+  return CE_GPU_OK;
+}
+
+int ce_gpu_ctx_profile(ce_gpu_ctx *ctx, int enable) {
+  if (!ctx) return fail(CE_GPU_EINVAL, "ctx is NULL");
+  ctx->profiling = enable != 0;
+  return CE_GPU_OK;
+}
+
+int ce_gpu_ctx_profile_read(ce_gpu_ctx *ctx, int kernel_class, double *total_ms, int64_t *launches) {
+  if (!ctx || kernel_class < 0 || kernel_class >= CE_GPU_PROF_CLASSES) return fail(CE_GPU_EINVAL, "bad argument");
+  CE_HIP(hipStreamSynchronize(ctx->stream));
+  double ms = 0.0;
+  int64_t n = 0;
+  std::vector<ce_gpu_ctx::Timed> keep;
+  for (const ce_gpu_ctx::Timed &t : ctx->timed) {
+    if (t.cls != kernel_class) {
+      keep.push_back(t);
+      continue;
+    }
+    float e = 0.0f;
+    CE_HIP(hipEventElapsedTime(&e, t.a, t.b));
+    ms += e;
+    ++n;
+    ctx->event_pool.push_back(t.a);
+    ctx->event_pool.push_back(t.b);
+  }
+  ctx->timed.swap(keep);
+  if (total_ms) *total_ms = ms;
+  if (launches) *launches = n;
+  return CE_GPU_OK;
+}
+
+int ce_gpu_model_load(ce_gpu_ctx *ctx, const char *nnet_path, const char *prior_path, int left_context,
+                      int right_context, ce_gpu_model **out) {
+  if (!ctx || !nnet_path || !prior_path || !out) return fail(CE_GPU_EINVAL, "NULL argument");
+  *out = nullptr;
+  return load_model(ctx, nnet_path, prior_path, left_context, right_context, "", out);
+}
+
+int ce_gpu_model_load_config(ce_gpu_ctx *ctx, const char *config_path, ce_gpu_model **out) {
+  if (!ctx || !config_path || !out) return fail(CE_GPU_EINVAL, "NULL argument");
+  *out = nullptr;
+  Config cf;
+  CE_TRY(cf.read(config_path));
+  std::string nnet, prior, tid2pdf;
+  int left = 0, right = 0, chunk = 0, num_pdfs = 0;
+  CE_TRY(cf.path("nnet", &nnet));
+  CE_TRY(cf.path("prior", &prior));
+  CE_TRY(cf.integer("left_context", &left));
+  CE_TRY(cf.integer("right_context", &right));
+  CE_TRY(cf.integer("chunk_size", &chunk));
+  CE_TRY(cf.integer("num_pdfs", &num_pdfs));
+  CE_TRY(cf.path("tid2pdf", &tid2pdf));
+  ce_gpu_model *m = nullptr;
+  CE_TRY(load_model(ctx, nnet, prior, left, right, tid2pdf, &m));
+  m->chunk = chunk;
+  *out = m;
+  return CE_GPU_OK;
+}
+
+int ce_gpu_model_info(const ce_gpu_model *m, int *left_context, int *right_context, int *input_dim,
+                      int *num_pdfs, int *num_linear, int64_t *num_params) {
+  if (!m) return fail(CE_GPU_EINVAL, "model is NULL");
+  if (left_context) *left_context = m->left;
+  if (right_context) *right_context = m->right;
+  if (input_dim) *input_dim = m->input_dim;
+  if (num_pdfs) *num_pdfs = m->num_pdfs;
+  if (num_linear) *num_linear = m->num_linear;
+  if (num_params) *num_params = m->num_params;
+  return CE_GPU_OK;
+}
+
+int ce_gpu_model_tid2pdf(const ce_gpu_model *m, int32_t *h_out, int capacity, int *size) {
+  if (!m) return fail(CE_GPU_EINVAL, "model is NULL");
+  const int n = (int)m->tid2pdf.size();
+  if (size) *size = n;
+  if (h_out && capacity > 0) memcpy(h_out, m->tid2pdf.data(), sizeof(int32_t) * std::min(n, capacity));
+  return CE_GPU_OK;
+}
+
+int ce_gpu_model_destroy(ce_gpu_model *m) {
+  delete m;
+  return CE_GPU_OK;
+}
+
+int64_t ce_gpu_fbank_num_frames(int64_t n) {
+  return n < kWinLen ? 0 : 1 + (n - kWinLen) / kShift;
+}
+
+int ce_gpu_plan_create(ce_gpu_ctx *ctx, const ce_gpu_model *model, const int64_t *h_num_samples, int n_utt,
+                       int max_rows, ce_gpu_plan **out) {
+  if (!ctx || !out || n_utt < 0 || (n_utt > 0 && !h_num_samples)) return fail(CE_GPU_EINVAL, "bad argument");
+  *out = nullptr;
+  CE_HIP(hipSetDevice(ctx->device));
+  std::unique_ptr<ce_gpu_plan> p(new (std::nothrow) ce_gpu_plan());
+  if (!p) return fail(CE_GPU_ENOMEM, "out of host memory");
+  p->n_utt = n_utt;
+  p->sample_off.assign(n_utt + 1, 0);
+  p->frame_off.assign(n_utt + 1, 0);
+  for (int u = 0; u < n_utt; ++u) {
+    if (h_num_samples[u] < 0) return fail(CE_GPU_EINVAL, "negative sample count");
+    p->sample_off[u + 1] = p->sample_off[u] + h_num_samples[u];
+    p->frame_off[u + 1] = p->frame_off[u] + ce_gpu_fbank_num_frames(h_num_samples[u]);
+  }
+  p->total_samples = p->sample_off[n_utt];
+  p->total_frames = p->frame_off[n_utt];
+  if (p->total_frames >= (int64_t)INT32_MAX) return fail(CE_GPU_EINVAL, "too many frames in one plan");
+  // fbank block -> first utterance
+  const int fpb = fbank_frames_per_block();
+  const int64_t blocks = (p->total_frames + fpb - 1) / fpb;
+  std::vector<int32_t> block_utt(std::max<int64_t>(blocks, 1), 0);
+  {
+    int u = 0;
+    for (int64_t b = 0; b < blocks; ++b) {
+      while (p->frame_off[u + 1] <= b * fpb) ++u;
+      block_utt[b] = u;
+    }
+  }
+  p->fbank_blocks = (int)blocks;
+  CE_TRY(p->d_sample_off.upload(p->sample_off.data(), p->sample_off.size() * 8));
+  CE_TRY(p->d_frame_off.upload(p->frame_off.data(), p->frame_off.size() * 8));
+  CE_TRY(p->d_block_utt.upload(block_utt.data(), block_utt.size() * 4));
+
+  if (model) {
+    const int L = model->left, R = model->right;
+    if (max_rows <= 0) max_rows = 4096;
+    if (max_rows < L + R + 1) return fail(CE_GPU_EINVAL, "max_rows smaller than the nnet context");
+    p->has_model = true;
+    p->left = L;
+    p->right = R;
+    std::vector<int32_t> src, dst;
+    ce_gpu_plan::Chunk cur;
+    auto close = [&]() {
+      if (cur.rows > 0) {
+        p->max_chunk_rows = std::max(p->max_chunk_rows, cur.rows);
+        p->chunks.push_back(cur);
+      }
+      cur = ce_gpu_plan::Chunk();
+      cur.map_base = (int64_t)src.size();
+    };
+    cur.map_base = 0;
+    for (int u = 0; u < n_utt; ++u) {
+      const int64_t T = p->frame_off[u + 1] - p->frame_off[u];
+      int64_t t = 0;
+      while (t < T) {
+        int64_t room = max_rows - cur.rows - L - R;
+        if (room < T - t && cur.rows > 0) {  // start the utterance in a fresh chunk
+          close();
+          room = max_rows - L - R;
+        }
+        const int64_t n = std::min(T - t, room);
+        for (int64_t j = 0; j < n + L + R; ++j) {
+          int64_t fr = t - L + j;
+          fr = fr < 0 ? 0 : (fr > T - 1 ? T - 1 : fr);
+          src.push_back((int32_t)(p->frame_off[u] + fr));
+          dst.push_back(j >= L && j < L + n ? (int32_t)(p->frame_off[u] + t + j - L) : -1);
+        }
+        cur.rows += (int)(n + L + R);
+        t += n;
+      }
+    }
+    close();
+    if (!src.empty()) {
+      CE_TRY(p->d_row_src.upload(src.data(), src.size() * 4));
+      CE_TRY(p->d_row_dst.upload(dst.data(), dst.size() * 4));
+    }
+  }
+  *out = p.release();
+  return CE_GPU_OK;
+}
+
+int ce_gpu_plan_info(const ce_gpu_plan *p, int *n_utt, int64_t *total_samples, int64_t *total_frames,
+                     int *n_chunks, int *max_chunk_rows) {
+  if (!p) return fail(CE_GPU_EINVAL, "plan is NULL");
+  if (n_utt) *n_utt = p->n_utt;
+  if (total_samples) *total_samples = p->total_samples;
+  if (total_frames) *total_frames = p->total_frames;
+  if (n_chunks) *n_chunks = (int)p->chunks.size();
+  if (max_chunk_rows) *max_chunk_rows = p->max_chunk_rows;
+  return CE_GPU_OK;
+}
+
+int ce_gpu_plan_frame_offsets(const ce_gpu_plan *p, int64_t *h_out) {
+  if (!p || !h_out) return fail(CE_GPU_EINVAL, "NULL argument");
+  memcpy(h_out, p->frame_off.data(), sizeof(int64_t) * p->frame_off.size());
+  return CE_GPU_OK;
+}
+
+int ce_gpu_plan_destroy(ce_gpu_plan *p) {
+  delete p;
+  return CE_GPU_OK;
+}
+
+int ce_gpu_fbank(ce_gpu_ctx *ctx, const ce_gpu_plan *p, const float *d_pcm, float *d_feats, float *d_mel) {
+  if (!ctx || !p || (p->total_frames > 0 && (!d_pcm || !d_feats))) return fail(CE_GPU_EINVAL, "NULL argument");
+  ProfScope prof(ctx, CE_GPU_PROF_FBANK);
+  return launch_fbank(ctx->stream, ctx->d_tables.as<FbankTables>(), p, d_pcm, d_feats, d_mel);
+}
+
+int ce_gpu_cmvn(ce_gpu_ctx *ctx, const ce_gpu_plan *p, const float *d_global_stats, const float *d_feats,
+                float *d_out) {
+  if (!ctx || !p || !d_global_stats || (p->total_frames > 0 && (!d_feats || !d_out)))
+    return fail(CE_GPU_EINVAL, "NULL argument");
+  const char *a = reinterpret_cast<const char *>(d_feats), *b = reinterpret_cast<const char *>(d_out);
+  const size_t bytes = (size_t)p->total_frames * kMel * sizeof(float);
+  if (bytes && a < b + bytes && b < a + bytes) return fail(CE_GPU_EINVAL, "cmvn: d_out overlaps d_feats");
+  ProfScope prof(ctx, CE_GPU_PROF_CMVN);
+  return launch_cmvn(ctx->stream, p, d_global_stats, d_feats, d_out);
+}
+
+int ce_gpu_am_forward(ce_gpu_ctx *ctx, const ce_gpu_model *m, const ce_gpu_plan *p, const float *d_feats,
+                      float *d_loglik) {
+  if (!ctx || !m || !p) return fail(CE_GPU_EINVAL, "NULL argument");
+  if (!p->has_model || p->left != m->left || p->right != m->right)
+    return fail(CE_GPU_EINVAL, "plan was not built for this model's context");
+  if (p->chunks.empty()) return CE_GPU_OK;
+  if (!d_feats || !d_loglik) return fail(CE_GPU_EINVAL, "NULL argument");
+  const size_t per = (size_t)p->max_chunk_rows * m->max_width;
+  CE_TRY(ensure_workspace(ctx, 2 * per));
+  float *buf[2] = {ctx->workspace.as<float>(), ctx->workspace.as<float>() + per};
+  for (const ce_gpu_plan::Chunk &c : p->chunks) {
+    const int *row_src = p->d_row_src.as<int>() + c.map_base;
+    const int *row_dst = p->d_row_dst.as<int>() + c.map_base;
+    const float *x = d_feats;
+    int ldx = m->input_dim, cur = 0;
+    bool first = true;
+    for (const Step &st : m->steps) {
+      if (st.is_gemm) {
+        const GemmLayer &g = st.gemm;
+        GemmArgs a;
+        a.x = x;
+        a.ldx = ldx;
+        a.row_map = first ? row_src : nullptr;
+        a.m = c.rows;
+        a.n = g.n;
+        a.k = g.k;
+        a.kpad = g.kpad;
+        a.din = g.din;
+        a.nseg = g.nseg;
+        for (int i = 0; i < 8; ++i) a.off[i] = g.off[i];
+        a.w = g.wt.as<float>();
+        a.ldw = g.kpad;
+        a.bias = g.bias.as<float>();
+        a.bn_scale = g.bn_scale.as<float>();
+        a.bn_offset = g.bn_offset.as<float>();
+        for (int i = 0; i < 4; ++i) a.post[i] = g.post[i];
+        a.npost = g.npost;
+        a.y = buf[cur];
+        a.ldy = g.n;
+        {
+          ProfScope prof(ctx, g.din % 32 == 0 ? CE_GPU_PROF_GEMM : CE_GPU_PROF_GEMM_GATHER);
+          CE_TRY(launch_gemm_f32(ctx->stream, a));
+        }
+        x = buf[cur];
+        ldx = g.n;
+        cur ^= 1;
+        first = false;
+      } else {
+        CE_TRY(launch_rowop(ctx->stream, st.row, const_cast<float *>(x), ldx, c.rows));
+      }
+    }
+    ProfScope prof(ctx, CE_GPU_PROF_FINALIZE);
+    CE_TRY(launch_finalize(ctx->stream, x, ldx, c.rows, m->num_pdfs, m->final_log_softmax,
+                           m->log_prior.as<float>(), row_dst, d_loglik));
+  }
+  return CE_GPU_OK;
+}
+
+int ce_gpu_score(ce_gpu_ctx *ctx, const ce_gpu_model *m, const ce_gpu_plan *p, const float *d_pcm,
+                 const float *d_global_stats, float *d_feats_ws, float *d_loglik) {
+  if (!ctx || !m || !p) return fail(CE_GPU_EINVAL, "NULL argument");
+  if (m->input_dim != kMel) return fail(CE_GPU_EINVAL, "nnet input is not 40-dim fbank");
+  CE_TRY(ce_gpu_fbank(ctx, p, d_pcm, d_feats_ws, nullptr));
+  const float *feats = d_feats_ws;
+  if (d_global_stats) {
+    float *norm = d_feats_ws + (size_t)p->total_frames * kMel;
+    CE_TRY(ce_gpu_cmvn(ctx, p, d_global_stats, d_feats_ws, norm));
+    feats = norm;
+  }
+  return ce_gpu_am_forward(ctx, m, p, feats, d_loglik);
+}
+
+int ce_gpu_sgemm(ce_gpu_ctx *ctx, int m, int n, int k, const float *d_a, int lda, const float *d_b, int ldb,
+                 float *d_c, int ldc) {
+  if (!ctx || m < 0 || n < 0 || k < 0) return fail(CE_GPU_EINVAL, "bad argument");
+  if (m == 0 || n == 0) return CE_GPU_OK;
+  if (k == 0) {
+    for (int i = 0; i < m; ++i) CE_HIP(hipMemsetAsync(d_c + (size_t)i * ldc, 0, sizeof(float) * n, ctx->stream));
+    return CE_GPU_OK;
+  }
+  if (lda < k || ldb < n || ldc < n) return fail(CE_GPU_EINVAL, "leading dimension too small");
+  GemmArgs a;
+  a.x = d_a;
+  a.ldx = lda;
+  a.m = m;
+  a.n = n;
+  a.k = k;
+  a.kpad = (k + 31) / 32 * 32;
+  a.din = k;
+  a.nseg = 1;
+  a.w = d_b;
+  a.ldw = ldb;
+  a.b_nmajor = true;
+  a.y = d_c;
+  a.ldy = ldc;
+  return launch_gemm_f32(ctx->stream, a);
+}
+
+int ce_gpu_quantize(ce_gpu_ctx *ctx, const float *d_x, int64_t count, uint8_t *d_q, void *d_params) {
+  if (!ctx || !d_x || !d_q || !d_params) return fail(CE_GPU_EINVAL, "NULL argument");
+  CE_TRY(ensure_scratch(ctx, 1024 * 8));
+  return launch_quantize(ctx->stream, d_x, count, d_q, d_params, ctx->scratch.ptr);
+}
+
+static int gemm_u8(ce_gpu_ctx *ctx, int m, int n, int k, const uint8_t *d_a, const void *d_pa,
+                   const uint8_t *d_b, const void *d_pb, float *d_cf, int32_t *d_ci) {
+  if (!ctx || !d_a || !d_pa || !d_b || !d_pb || (!d_cf && !d_ci)) return fail(CE_GPU_EINVAL, "NULL argument");
+  if (m <= 0 || n <= 0 || k <= 0) return fail(CE_GPU_EINVAL, "gemm_u8: empty operand (reference asserts)");
+  CE_TRY(ensure_scratch(ctx, gemm_u8_scratch_bytes(m, n, k)));
+  return launch_gemm_u8_ws(ctx->stream, m, n, k, d_a, d_pa, d_b, d_pb, d_cf, d_ci, ctx->scratch.ptr);
+}
+
+int ce_gpu_gemm_u8u8f32(ce_gpu_ctx *ctx, int m, int n, int k, const uint8_t *d_a, const void *d_params_a,
+                        const uint8_t *d_b, const void *d_params_b, float *d_c) {
+  return gemm_u8(ctx, m, n, k, d_a, d_params_a, d_b, d_params_b, d_c, nullptr);
+}
+
+int ce_gpu_gemm_u8u8i32(ce_gpu_ctx *ctx, int m, int n, int k, const uint8_t *d_a, const void *d_params_a,
+                        const uint8_t *d_b, const void *d_params_b, int32_t *d_c) {
+  return gemm_u8(ctx, m, n, k, d_a, d_params_a, d_b, d_params_b, nullptr, d_c);
+}
+
+}  // extern "C"

@@ -1,0 +1,149 @@
+// fbank_ops.h -- per-lane arithmetic of the fbank kernel, shared verbatim by
+// the device kernel (kernels/fbank.hip) and the CPU schedule emulator used in
+// tests (tests/native/emu_fbank.cc), so the emulator proves on a CPU that the
+// lane decomposition reproduces the reference's float operations exactly.
+//
+// Every expression keeps the reference's operation order and roundings; the
+// translation units that include this header are compiled with
+// -ffp-contract=off so no multiply-add is fused (the reference runs on x86-64
+// without FMA).
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define CE_HD __host__ __device__ __forceinline__
+#else
+#define CE_HD static inline
+#endif
+
+namespace catears {
+namespace fb {
+
+// Pre-emphasis of one sample in double (src/fbank.cc:57-61: PK_PREEMPH_COEFF
+// is the double literal 0.97, `x[i] -= 0.97 * x[i-1]` on a float lvalue).
+CE_HD float preemph(float cur, float prev) {
+  const double p = 0.97 * (double)prev;
+  return (float)((double)cur - p);
+}
+
+// One lane op of the split-radix generation schedule (src/srfft.cc:124-265).
+// op = kind(2) | lg(4) | n(8) | base(8); see tables.cc build_fft_schedule.
+CE_HD void fft_lane_op(uint32_t op, float *re, float *im, const float *twiddle,
+                       const int *twiddle_base) {
+  const uint32_t kind = op & 3u;
+  if (kind == 0u) return;
+  const int lg = (int)((op >> 2) & 15u), n = (int)((op >> 6) & 255u), base = (int)(op >> 14);
+  float t1, t2;
+  if (kind == 3u) {  // length-2 node (srfft.cc:206-216)
+    float *r = re + base, *i = im + base;
+    t1 = r[0] + r[1]; r[1] = r[0] - r[1]; r[0] = t1;
+    t1 = i[0] + i[1]; i[1] = i[0] - i[1]; i[0] = t1;
+    return;
+  }
+  if (kind == 2u) {  // length-4 node (srfft.cc:163-205)
+    float *r = re + base, *i = im + base;
+    t1 = r[0] + r[2]; r[2] = r[0] - r[2]; r[0] = t1;
+    t1 = i[0] + i[2]; i[2] = i[0] - i[2]; i[0] = t1;
+    t1 = r[1] + r[3]; r[3] = r[1] - r[3]; r[1] = t1;
+    t1 = i[1] + i[3]; i[3] = i[1] - i[3]; i[1] = t1;
+    t1 = r[0] + r[1]; r[1] = r[0] - r[1]; r[0] = t1;
+    t1 = i[0] + i[1]; i[1] = i[0] - i[1]; i[0] = t1;
+    t1 = r[2] + i[3];
+    t2 = i[2] + r[3];
+    i[2] = i[2] - r[3];
+    r[3] = r[2] - i[3];
+    r[2] = t1;
+    i[3] = t2;
+    return;
+  }
+  // general node of length m = 2^lg: this lane owns n, n+q, n+h, n+h+q
+  const int q = 1 << (lg - 2), h = 2 * q, e = q / 2;
+  const int p0 = base + n, p1 = p0 + q, p2 = p0 + h, p3 = p2 + q;
+  float ar = re[p0], ai = im[p0], br = re[p1], bi = im[p1];
+  float cr = re[p2], ci = im[p2], dr = re[p3], di = im[p3];
+  // step 1: butterflies (n, n+h) and (n+q, n+q+h)
+  t1 = ar + cr; cr = ar - cr; ar = t1;
+  t1 = ai + ci; ci = ai - ci; ai = t1;
+  t1 = br + dr; dr = br - dr; br = t1;
+  t1 = bi + di; di = bi - di; bi = t1;
+  // step 2: (h+n, h+q+n)
+  t1 = cr + di;
+  t2 = ci + dr;
+  ci = ci - dr;
+  dr = cr - di;
+  cr = t1;
+  di = t2;
+  // steps 3 & 4: twiddles for n >= 1
+  if (n == e) {
+    const float sq = (float)0.70710678118654752440;
+    t1 = sq * (cr + ci);
+    ci = sq * (ci - cr);
+    cr = t1;
+    t2 = sq * (di - dr);
+    di = -sq * (dr + di);
+    dr = t2;
+  } else if (n > 0) {
+    const int nel = q - 2, w = n - 1 - (n > e ? 1 : 0);
+    const float *tw = twiddle + twiddle_base[lg];
+    t2 = tw[w] * (cr + ci);
+    t1 = tw[nel + w] * cr + t2;
+    cr = tw[2 * nel + w] * ci + t2;
+    ci = t1;
+    t2 = tw[3 * nel + w] * (dr + di);
+    t1 = tw[4 * nel + w] * dr + t2;
+    dr = tw[5 * nel + w] * di + t2;
+    di = t1;
+  }
+  re[p0] = ar; im[p0] = ai; re[p1] = br; im[p1] = bi;
+  re[p2] = cr; im[p2] = ci; re[p3] = dr; im[p3] = di;
+}
+
+CE_HD int bitrev8(int k) {
+  int r = 0;
+  for (int b = 0; b < 8; ++b) r |= ((k >> b) & 1) << (7 - b);
+  return r;
+}
+
+// Real-FFT post-processing for one k in 1..128 (src/srfft.cc:382-438) fused
+// with the power spectrum (src/fbank.cc:193-211).  re/im hold the complex FFT
+// before its bit-reversal permutation, so B_k is read at bitrev(k).  Writes
+// power[k] and power[256-k].
+CE_HD void post_power(int k, const float *re, const float *im, const float *kn, float *power) {
+  const int kk = 256 - k;
+  const int a = bitrev8(k), b = bitrev8(kk & 255);
+  const float xr = re[a], xi = im[a], yr = re[b], yi = im[b];
+  const float kr = kn[2 * k], ki = kn[2 * k + 1];
+  // 0.5 * (float sum) in double then back to float == exact halving
+  const float c_re = (float)(0.5 * (double)(xr + yr));
+  const float c_im = (float)(0.5 * (double)(xi - yi));
+  const float d_re = (float)(0.5 * (double)(xi + yi));
+  const float d_im = (float)(-0.5 * (double)(xr - yr));
+  float o_re = c_re, o_im = c_im;
+  o_re += kr * d_re - ki * d_im;
+  o_im += kr * d_im + ki * d_re;
+  power[k] = o_re * o_re + o_im * o_im;
+  if (kk != k) {
+    float p_re = c_re, p_im = -c_im;
+    p_re += (-kr) * d_re - ki * (-d_im);
+    p_im += (-kr) * (-d_im) + ki * d_re;
+    power[kk] = p_re * p_re + p_im * p_im;
+  }
+}
+
+// DC / Nyquist bins (src/srfft.cc:446-451 then fbank.cc:203-204).
+CE_HD void edge_power(const float *re, const float *im, float *power) {
+  const float z = re[0] + im[0], nyq = re[0] - im[0];
+  power[0] = z * z;
+  power[256] = nyq * nyq;
+}
+
+// Melbanks::Compute for one bin: sequential float dot (src/vector.cc:81-92).
+CE_HD float mel_dot(const float *w, const float *p, int len) {
+  float e = 0.0f;
+  for (int i = 0; i < len; ++i) e += w[i] * p[i];
+  return e;
+}
+
+}  // namespace fb
+}  // namespace catears

@@ -1,0 +1,226 @@
+// internal.h -- private structures of libcatears_hip (not part of the ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "catears_gpu.h"
+
+namespace catears {
+
+// ---------------------------------------------------------------- errors --
+
+// Records `msg` as this thread's last error and returns `code`.
+int fail(int code, const std::string &msg);
+// HIP error -> CE_GPU_EHIP with context.
+int hip_fail(hipError_t e, const char *what);
+
+#define CE_HIP(expr)                                        \
+  do {                                                      \
+    hipError_t e_ = (expr);                                 \
+    if (e_ != hipSuccess) return ::catears::hip_fail(e_, #expr); \
+  } while (0)
+
+#define CE_TRY(expr)                 \
+  do {                               \
+    int rc_ = (expr);                \
+    if (rc_ != CE_GPU_OK) return rc_; \
+  } while (0)
+
+// ------------------------------------------------------- device buffers --
+
+// Owning device allocation (hipMalloc); never copied.
+struct DevBuf {
+  void *ptr = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf &) = delete;
+  DevBuf &operator=(const DevBuf &) = delete;
+  DevBuf(DevBuf &&o) noexcept : ptr(o.ptr), bytes(o.bytes) { o.ptr = nullptr, o.bytes = 0; }
+  DevBuf &operator=(DevBuf &&o) noexcept {
+    if (this != &o) {
+      release();
+      ptr = o.ptr, bytes = o.bytes;
+      o.ptr = nullptr, o.bytes = 0;
+    }
+    return *this;
+  }
+  ~DevBuf() { release(); }
+  int alloc(size_t n);
+  int upload(const void *src, size_t n);  // alloc + synchronous H2D copy
+  void release();
+  template <typename T>
+  T *as() const { return static_cast<T *>(ptr); }
+};
+
+// ------------------------------------------------------------ fbank tables --
+
+// Fixed fbank geometry (src/fbank.h:7-13).
+constexpr int kShift = 160;
+constexpr int kWinLen = 400;
+constexpr int kPadded = 512;
+constexpr int kHalf = 256;   // complex FFT points
+constexpr int kMel = 40;
+constexpr int kFftGens = 7;  // split-radix generations (see tables.cc)
+
+// Tables shared by every frame; built on the host by the reference's formulas
+// and uploaded once per context.  Layout is what kernels/fbank.hip indexes.
+struct FbankTables {
+  float window[kWinLen];            // Hamming, src/fbank.cc:248-255
+  float twiddle[6 * 64 * 5];        // levels 4..8, 6 x (m/4 - 2) each
+  int twiddle_base[9];              // start of level lg in `twiddle`
+  float kn[2 * 129];                // real-FFT post twiddles kN_k, k = 1..128
+  uint32_t fft_ops[kFftGens * 64];  // per generation, per lane node op
+  int mel_off[kMel];                // first FFT bin of each triangle
+  int mel_len[kMel];
+  int mel_wbase[kMel];              // start of its weights in mel_w
+  float mel_w[512];                 // 492 nonzero weights in total
+  int mel_total;
+};
+
+// Builds the tables (tables.cc).
+void build_fbank_tables(FbankTables *t);
+
+// Node-op encoding for fft_ops: kind(2) | lg(4) | n(8) | base(8).
+enum FftOpKind : uint32_t { kOpNone = 0, kOpNode = 1, kOpLeaf4 = 2, kOpLeaf2 = 3 };
+inline uint32_t fft_op(uint32_t kind, uint32_t lg, uint32_t n, uint32_t base) {
+  return kind | (lg << 2) | (n << 6) | (base << 14);
+}
+
+// -------------------------------------------------------------- nnet ops --
+
+// Post-ops fused into a GEMM epilogue (applied in order, up to 4).
+enum PostOp : int { kPostNone = 0, kPostRelu = 1, kPostBatchNorm = 2 };
+
+struct GemmLayer {
+  int din = 0;            // input row width (one splice segment)
+  int nseg = 1;           // splice indices (segments of the K dimension)
+  int off[8] = {0};       // row offset of each segment
+  int k = 0, kpad = 0, n = 0;
+  DevBuf wt;              // n x kpad, K-contiguous (transposed MAT0)
+  DevBuf bias;            // n
+  DevBuf bn_scale, bn_offset;  // n, when a BatchNorm is fused
+  int post[4] = {0, 0, 0, 0};
+  int npost = 0;
+};
+
+enum RowOpKind : int { kRowRelu, kRowBatchNorm, kRowLogSoftmax, kRowSoftmax, kRowNormalize };
+
+struct RowOp {
+  int kind = 0;
+  int dim = 0;
+  DevBuf scale, offset;  // BatchNorm
+};
+
+// One executable step of the nnet program.
+struct Step {
+  bool is_gemm = true;
+  GemmLayer gemm;
+  RowOp row;
+};
+
+}  // namespace catears
+
+// ------------------------------------------------------------ ABI objects --
+
+struct ce_gpu_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  catears::FbankTables host_tables;
+  catears::DevBuf d_tables;    // FbankTables image on device
+  catears::DevBuf workspace;   // nnet activations (grown on demand)
+  size_t workspace_floats = 0;
+  catears::DevBuf scratch;     // reductions / int8 operand staging (grown on demand)
+  // optional per-class launch timing (ce_gpu_ctx_profile)
+  bool profiling = false;
+  struct Timed {
+    int cls;
+    hipEvent_t a, b;
+  };
+  std::vector<Timed> timed;
+  std::vector<hipEvent_t> event_pool;
+};
+
+namespace catears {
+// Brackets one launch with events when ctx->profiling is set.
+struct ProfScope {
+  ce_gpu_ctx *ctx;
+  int cls;
+  hipEvent_t b = nullptr;
+  ProfScope(ce_gpu_ctx *c, int k);
+  ~ProfScope();
+};
+}  // namespace catears
+
+struct ce_gpu_model {
+  int left = 0, right = 0, chunk = 0;
+  int input_dim = 0, num_pdfs = 0, num_linear = 0, max_width = 0;
+  int64_t num_params = 0;
+  bool final_log_softmax = false;
+  std::vector<catears::Step> steps;  // all but the final log-softmax
+  catears::DevBuf log_prior;         // num_pdfs
+  std::vector<int32_t> tid2pdf;
+};
+
+struct ce_gpu_plan {
+  int n_utt = 0;
+  int64_t total_samples = 0, total_frames = 0;
+  std::vector<int64_t> sample_off, frame_off;  // n_utt + 1 each (host)
+  // fbank launch map: per block of kFramesPerBlock frames, first utterance
+  catears::DevBuf d_sample_off, d_frame_off, d_block_utt;
+  int fbank_blocks = 0;
+  // nnet chunks
+  struct Chunk {
+    int rows = 0;          // packed rows (<= max_rows)
+    int64_t map_base = 0;  // offset into d_row_src / d_row_dst
+  };
+  std::vector<Chunk> chunks;
+  catears::DevBuf d_row_src;  // int32 per packed row: source feature row
+  catears::DevBuf d_row_dst;  // int32 per packed row: output row or -1
+  int max_chunk_rows = 0;
+  int left = 0, right = 0;
+  bool has_model = false;
+};
+
+namespace catears {
+
+// Kernel launchers (kernels/*.hip).  All enqueue on `s` and return a status.
+int launch_fbank(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, const float *pcm,
+                 float *feats, float *mel);
+int launch_cmvn(hipStream_t s, const ce_gpu_plan *p, const float *gstats, const float *in,
+                float *out);
+
+struct GemmArgs {
+  const float *x = nullptr;   // A source rows
+  int ldx = 0;
+  const int *row_map = nullptr;  // optional: packed row -> source row of x
+  int m = 0, n = 0, k = 0, kpad = 0;
+  int din = 0, nseg = 1;
+  int off[8] = {0};
+  const float *w = nullptr;   // B: n x kpad (K-major) or k x ldw (N-major)
+  int ldw = 0;
+  bool b_nmajor = false;
+  const float *bias = nullptr, *bn_scale = nullptr, *bn_offset = nullptr;
+  int post[4] = {0, 0, 0, 0};
+  int npost = 0;
+  float *y = nullptr;
+  int ldy = 0;
+};
+int launch_gemm_f32(hipStream_t s, const GemmArgs &a);
+
+// Final step: optional log-softmax per row, minus log prior, scatter to the
+// output rows named by row_dst (-1 = drop).
+int launch_finalize(hipStream_t s, const float *x, int ldx, int rows, int dim, bool log_softmax,
+                    const float *log_prior, const int *row_dst, float *out);
+int launch_rowop(hipStream_t s, const RowOp &op, float *x, int ldx, int rows);
+
+int launch_quantize(hipStream_t s, const float *x, int64_t count, uint8_t *q, void *params,
+                    void *scratch);
+size_t gemm_u8_scratch_bytes(int m, int n, int k);
+int launch_gemm_u8_ws(hipStream_t s, int m, int n, int k, const uint8_t *a, const void *pa,
+                      const uint8_t *b, const void *pb, float *c_f32, int32_t *c_i32, void *ws);
+
+}  // namespace catears

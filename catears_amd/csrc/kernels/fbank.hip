@@ -1,0 +1,144 @@
+// fbank.hip -- batched log-mel filterbank on gfx950.
+//
+// Replaces the per-frame loop of Fbank::Process (src/fbank.cc:297-303):
+// ExtractWindow + ProcessWindow (fbank.cc:44-100), SRFFT::Compute
+// (srfft.cc:370-459), ComputePowerSpectrum (fbank.cc:193-211),
+// Melbanks::Compute (fbank.cc:165-184), floor + log (fbank.cc:243-244).
+//
+// Mapping: one wave (64 lanes) per frame, four frames per 256-thread block,
+// frames of every utterance of the batch flattened into one grid.
+//   1. the frame's 400 samples are read once from HBM (7 coalesced loads per
+//      lane), the DC mean is a wave reduction;
+//   2. pre-emphasis (double, as the reference) and the Hamming window are
+//      applied while scattering even/odd samples into the wave's complex
+//      re/im arrays in LDS (the real->complex packing of srfft.cc:318-324);
+//   3. the 256-point split-radix complex FFT runs as 7 generations of lane
+//      ops (tables.cc), each lane op touching 4 points in registers;
+//   4. real-FFT post-pass + power spectrum for two k per lane, reading the
+//      FFT output at bit-reversed positions instead of permuting it;
+//   5. lanes 0..39 each form one mel energy (sequential dot, as the
+//      reference), floor at FLT_EPSILON, logf, and store one row of 40 floats.
+// Everything up to the final logf is the reference's float arithmetic in the
+// reference's order (the DC sum is exact for integer-valued PCM, whose partial
+// sums are integers below 2^24), so pre-log mel energies match bit for bit.
+#include <float.h>
+#include <hip/hip_runtime.h>
+
+#include "../fbank_ops.h"
+#include "../internal.h"
+
+namespace catears {
+namespace {
+
+constexpr int kFramesPerBlock = 4;
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+struct WaveSmem {
+  float x[kWinLen];   // mean-removed samples, later the power spectrum
+  float re[kHalf];
+  float im[kHalf];
+};
+
+__global__ __launch_bounds__(256) void fbank_kernel(const FbankTables *__restrict__ tab,
+                                                    const float *__restrict__ pcm,
+                                                    const int64_t *__restrict__ sample_off,
+                                                    const int64_t *__restrict__ frame_off,
+                                                    const int *__restrict__ block_utt,
+                                                    int64_t total_frames, float *__restrict__ feats,
+                                                    float *__restrict__ mel_out) {
+  __shared__ WaveSmem smem[kFramesPerBlock];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t f = (int64_t)blockIdx.x * kFramesPerBlock + wave;
+  if (f >= total_frames) return;  // whole wave leaves; no block barrier below
+  WaveSmem &S = smem[wave];
+
+  int u = block_utt[blockIdx.x];
+  while (f >= frame_off[u + 1]) ++u;
+  const float *src = pcm + sample_off[u] + (f - frame_off[u]) * kShift;
+
+  // 1. samples + DC offset
+  float v[7];
+  float part = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    const int i = lane + 64 * j;
+    v[j] = i < kWinLen ? src[i] : 0.0f;
+    part += v[j];
+  }
+  const float mean = wave_sum(part) / (float)kWinLen;
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    const int i = lane + 64 * j;
+    if (i < kWinLen) S.x[i] = v[j] - mean;
+  }
+  wave_sync();
+
+  // 2. pre-emphasis, window, pack even/odd samples as re/im, zero pad
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    const int i = lane + 64 * j;
+    if (i < kWinLen) {
+      const float cur = S.x[i];
+      const float prev = i > 0 ? S.x[i - 1] : cur;
+      const float y = fb::preemph(cur, prev) * tab->window[i];
+      if (i & 1)
+        S.im[i >> 1] = y;
+      else
+        S.re[i >> 1] = y;
+    }
+  }
+  if (lane < kHalf - kWinLen / 2) {
+    S.re[kWinLen / 2 + lane] = 0.0f;
+    S.im[kWinLen / 2 + lane] = 0.0f;
+  }
+  wave_sync();
+
+  // 3. split-radix generations
+#pragma unroll 1
+  for (int g = 0; g < kFftGens; ++g) {
+    fb::fft_lane_op(tab->fft_ops[g * 64 + lane], S.re, S.im, tab->twiddle, tab->twiddle_base);
+    wave_sync();
+  }
+
+  // 4. real-FFT post-pass + power spectrum into S.x[0..256]
+  fb::post_power(lane + 1, S.re, S.im, tab->kn, S.x);
+  fb::post_power(lane + 65, S.re, S.im, tab->kn, S.x);
+  if (lane == 0) fb::edge_power(S.re, S.im, S.x);
+  wave_sync();
+
+  // 5. mel energies, floor, log
+  if (lane < kMel) {
+    const float e = fb::mel_dot(tab->mel_w + tab->mel_wbase[lane], S.x + tab->mel_off[lane],
+                                tab->mel_len[lane]);
+    if (mel_out) mel_out[f * kMel + lane] = e;
+    feats[f * kMel + lane] = logf(e < FLT_EPSILON ? FLT_EPSILON : e);
+  }
+}
+
+}  // namespace
+
+int launch_fbank(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, const float *pcm,
+                 float *feats, float *mel) {
+  if (p->total_frames == 0) return CE_GPU_OK;
+  const int64_t blocks = (p->total_frames + kFramesPerBlock - 1) / kFramesPerBlock;
+  hipLaunchKernelGGL(fbank_kernel, dim3((unsigned)blocks), dim3(256), 0, s, d_tab, pcm,
+                     p->d_sample_off.as<int64_t>(), p->d_frame_off.as<int64_t>(),
+                     p->d_block_utt.as<int>(), p->total_frames, feats, mel);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
+int fbank_frames_per_block() { return kFramesPerBlock; }
+
+}  // namespace catears

@@ -1,0 +1,136 @@
+// rowops.hip -- per-row kernels of the nnet path.
+//
+// finalize: LogSoftmaxLayer (src/nnet.cc:137-146 -> ApplyLogSoftMax,
+//   src/vector.cc:109-122: x - log(sum exp x), no max shift) fused with the
+//   log-prior subtraction of AcousticModel::ComputeBatch (src/am.cc:108-112)
+//   and the scatter of valid packed rows to their utterance's output rows.
+//   One wave per row; the row is read once into registers.
+// rowop: stand-alone ReLU / BatchNorm / Softmax / LogSoftmax / Normalize for
+//   layers that do not directly follow a LinearLayer (never emitted by the
+//   reference's converter, but legal NN02).
+#include <hip/hip_runtime.h>
+
+#include "../internal.h"
+
+namespace catears {
+namespace {
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+constexpr int kMaxPerLane = 64;  // rows up to 4096 wide stay in registers
+
+template <bool LOGSM>
+__global__ __launch_bounds__(256) void finalize_kernel(const float *__restrict__ x, int ldx, int rows,
+                                                       int dim, const float *__restrict__ prior,
+                                                       const int *__restrict__ row_dst,
+                                                       float *__restrict__ out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int dst = row_dst ? row_dst[row] : row;
+  if (dst < 0) return;
+  const float *xr = x + (int64_t)row * ldx;
+  float *o = out + (int64_t)dst * dim;
+  if (dim <= 64 * kMaxPerLane) {
+    float v[kMaxPerLane];
+    float s = 0.0f;
+#pragma unroll
+    for (int j = 0; j < kMaxPerLane; ++j) {
+      const int c = lane + 64 * j;
+      v[j] = c < dim ? xr[c] : 0.0f;
+      if (LOGSM && c < dim) s += expf(v[j]);
+    }
+    const float ls = LOGSM ? logf(wave_sum(s)) : 0.0f;
+#pragma unroll
+    for (int j = 0; j < kMaxPerLane; ++j) {
+      const int c = lane + 64 * j;
+      if (c < dim) {
+        float y = v[j];
+        if (LOGSM) y = y - ls;
+        o[c] = y - prior[c];
+      }
+    }
+  } else {
+    float s = 0.0f;
+    if (LOGSM)
+      for (int c = lane; c < dim; c += 64) s += expf(xr[c]);
+    const float ls = LOGSM ? logf(wave_sum(s)) : 0.0f;
+    for (int c = lane; c < dim; c += 64) {
+      float y = xr[c];
+      if (LOGSM) y = y - ls;
+      o[c] = y - prior[c];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void rowop_kernel(int kind, float *__restrict__ x, int ldx, int rows,
+                                                    int dim, const float *__restrict__ scale,
+                                                    const float *__restrict__ offset) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  float *xr = x + (int64_t)row * ldx;
+  switch (kind) {
+    case kRowRelu:  // nnet.cc:149-160
+      for (int c = lane; c < dim; c += 64) xr[c] = xr[c] < 0.0f ? 0.0f : xr[c];
+      break;
+    case kRowBatchNorm:  // nnet.cc:106-117: MulElements then AddVec(1.0)
+      for (int c = lane; c < dim; c += 64) {
+        float v = xr[c] * scale[c];
+        xr[c] = v + offset[c];
+      }
+      break;
+    case kRowLogSoftmax: {  // vector.cc:109-122
+      float s = 0.0f;
+      for (int c = lane; c < dim; c += 64) s += expf(xr[c]);
+      const float ls = logf(wave_sum(s));
+      for (int c = lane; c < dim; c += 64) xr[c] = xr[c] - ls;
+      break;
+    }
+    case kRowSoftmax: {  // vector.cc:94-107
+      float s = 0.0f;
+      for (int c = lane; c < dim; c += 64) s += expf(xr[c]);
+      s = wave_sum(s);
+      for (int c = lane; c < dim; c += 64) xr[c] = expf(xr[c]) / s;
+      break;
+    }
+    case kRowNormalize: {  // nnet.cc:163-178
+      float s = 0.0f;
+      for (int c = lane; c < dim; c += 64) s += xr[c] * xr[c];
+      s = wave_sum(s);
+      const float sc = (float)sqrt((double)(float)dim / (double)s);
+      for (int c = lane; c < dim; c += 64) xr[c] = xr[c] * sc;
+      break;
+    }
+    default:
+      break;
+  }
+}
+
+}  // namespace
+
+int launch_finalize(hipStream_t s, const float *x, int ldx, int rows, int dim, bool log_softmax,
+                    const float *log_prior, const int *row_dst, float *out) {
+  if (rows <= 0) return CE_GPU_OK;
+  dim3 grid((rows + 3) / 4), block(256);
+  if (log_softmax)
+    hipLaunchKernelGGL(finalize_kernel<true>, grid, block, 0, s, x, ldx, rows, dim, log_prior,
+                       row_dst, out);
+  else
+    hipLaunchKernelGGL(finalize_kernel<false>, grid, block, 0, s, x, ldx, rows, dim, log_prior,
+                       row_dst, out);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
+int launch_rowop(hipStream_t s, const RowOp &op, float *x, int ldx, int rows) {
+  if (rows <= 0) return CE_GPU_OK;
+  hipLaunchKernelGGL(rowop_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, op.kind, x, ldx, rows,
+                     op.dim, op.scale.as<float>(), op.offset.as<float>());
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
+}  // namespace catears

@@ -1,0 +1,161 @@
+// tables.cc -- host-built constant tables of the fbank kernel.
+//
+// Every value is produced with the reference's own formula and precision on
+// the host (glibc libm), then uploaded once, so the device never evaluates a
+// transcendental for a table entry and the window / twiddles / mel weights are
+// bit-identical to the reference's:
+//   Hamming window        src/fbank.cc:248-255 (2*pi truncated to 6.28318530718,
+//                         src/fbank.cc:18-20; cos(float) -> cosf)
+//   mel triangles         src/fbank.cc:103-163 (all float; MelScale uses logf)
+//   split-radix twiddles  src/srfft.cc:74-122 (float angle, cosf/sinf)
+//   real-FFT post twiddle src/srfft.cc:382-392: kN_k = kN_{k-1} * rootN by a
+//                         float complex multiply (srfft.cc:52-56), tabled so
+//                         that the device can process every k in parallel.
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "internal.h"
+
+namespace catears {
+namespace {
+
+constexpr double kTwoPiSrfft = 6.283185307179586476925286766559005;  // srfft.cc:37
+constexpr double kTwoPiFbank = 6.28318530718;                          // fbank.cc:19
+
+float mel_of(float hz) { return 1127.0f * logf(1.0f + hz / 700.0f); }
+
+void build_window(FbankTables *t) {
+  const float step = (float)(kTwoPiFbank / (kWinLen - 1));
+  for (int i = 0; i < kWinLen; ++i) {
+    float c = cosf(step * (float)i);
+    t->window[i] = (float)(0.54 - 0.46 * (double)c);
+  }
+}
+
+void build_mel(FbankTables *t) {
+  const float bin_hz = 16000.0f / kPadded;
+  const float mlo = mel_of(20.0f), mhi = mel_of(8000.0f);
+  const float step = (mhi - mlo) / (kMel + 1);
+  int cursor = 0;
+  for (int b = 0; b < kMel; ++b) {
+    const float left = mlo + b * step, centre = mlo + (b + 1) * step, right = mlo + (b + 2) * step;
+    int first = -1;
+    std::vector<float> w;
+    for (int k = 0; k < kHalf; ++k) {
+      float m = mel_of(bin_hz * k);
+      if (!(m > left && m < right)) continue;
+      if (first < 0) first = k;
+      // zero entries inside the span keep their slot (contiguous weights)
+      w.resize(k - first + 1, 0.0f);
+      w[k - first] = m <= centre ? (m - left) / (centre - left) : (right - m) / (right - centre);
+    }
+    t->mel_off[b] = first;
+    t->mel_len[b] = (int)w.size();
+    t->mel_wbase[b] = cursor;
+    for (float v : w) t->mel_w[cursor++] = v;
+  }
+  t->mel_total = cursor;
+}
+
+void build_twiddles(FbankTables *t) {
+  int cursor = 0;
+  for (int lg = 0; lg < 9; ++lg) t->twiddle_base[lg] = 0;
+  for (int lg = 4; lg <= 8; ++lg) {
+    const int m = 1 << lg, q = m / 4, e = m / 8, nel = q - 2;
+    t->twiddle_base[lg] = cursor;
+    float *dst = t->twiddle + cursor;
+    int w = 0;
+    for (int n = 1; n < q; ++n) {
+      if (n == e) continue;
+      float a = (float)(n * kTwoPiSrfft / m);
+      float c = cosf(a), s = sinf(a);
+      dst[w] = c;
+      dst[nel + w] = -(s + c);
+      dst[2 * nel + w] = s - c;
+      a = (float)(3 * n * kTwoPiSrfft / m);
+      c = cosf(a);
+      s = sinf(a);
+      dst[3 * nel + w] = c;
+      dst[4 * nel + w] = -(s + c);
+      dst[5 * nel + w] = s - c;
+      ++w;
+    }
+    cursor += 6 * nel;
+  }
+}
+
+void build_post_twiddles(FbankTables *t) {
+  const float ang = (float)(kTwoPiSrfft / kPadded * -1);
+  const float rr = cosf(ang), ri = sinf(ang);
+  float kr = 1.0f, ki = 0.0f;
+  t->kn[0] = kr;
+  t->kn[1] = ki;
+  for (int k = 1; k <= kHalf / 2; ++k) {
+    float nr = (kr * rr) - (ki * ri);
+    ki = kr * ri + ki * rr;
+    kr = nr;
+    t->kn[2 * k] = kr;
+    t->kn[2 * k + 1] = ki;
+  }
+}
+
+// The split-radix recursion (srfft.cc:124-265) as a DAG of node ops.  A node
+// of length m = 2^lg (lg >= 3) becomes m/4 lane ops: lane n owns points n,
+// n+m/4, n+m/2, n+3m/4 and performs the node's step-1 butterflies, step-2
+// rotation and step-3/4 twiddles on them, in the reference's operation order.
+// Nodes of length 4 and 2 are one lane op each.  Independent ops are packed
+// into generations of <= 64 lanes (one wave); a node's children go to a later
+// generation than the node itself.
+struct Pending {
+  int lg, base, ready;
+};
+
+void build_fft_schedule(FbankTables *t) {
+  std::vector<std::vector<uint32_t>> gens(4 * kFftGens);
+  std::vector<Pending> pending = {{8, 0, 0}};
+  while (!pending.empty()) {
+    // earliest-ready first; among equals the longest node (deepest subtree),
+    // so leaves, which have no successors, absorb any generation overflow
+    size_t pick = 0;
+    for (size_t i = 1; i < pending.size(); ++i) {
+      const Pending &a = pending[i], &b = pending[pick];
+      if (a.ready < b.ready || (a.ready == b.ready && a.lg > b.lg)) pick = i;
+    }
+    Pending p = pending[pick];
+    pending.erase(pending.begin() + pick);
+    if (p.lg == 0) continue;
+    const int width = p.lg >= 3 ? (1 << p.lg) / 4 : 1;
+    int g = p.ready;
+    while ((int)gens[g].size() + width > 64) ++g;  // list scheduling
+    if (p.lg >= 3) {
+      for (int n = 0; n < width; ++n) gens[g].push_back(fft_op(kOpNode, p.lg, n, p.base));
+      const int m = 1 << p.lg;
+      pending.push_back({p.lg - 1, p.base, g + 1});
+      pending.push_back({p.lg - 2, p.base + m / 2, g + 1});
+      pending.push_back({p.lg - 2, p.base + 3 * (m / 4), g + 1});
+    } else {
+      gens[g].push_back(fft_op(p.lg == 2 ? kOpLeaf4 : kOpLeaf2, p.lg, 0, p.base));
+    }
+  }
+  for (size_t g = kFftGens; g < gens.size(); ++g)
+    if (!gens[g].empty()) abort();  // schedule must fit kFftGens generations
+  for (int g = 0; g < kFftGens; ++g)
+    for (int l = 0; l < 64; ++l)
+      t->fft_ops[g * 64 + l] = l < (int)gens[g].size() ? gens[g][l] : fft_op(kOpNone, 0, 0, 0);
+}
+
+}  // namespace
+
+void build_fbank_tables(FbankTables *t) {
+  memset(t, 0, sizeof(*t));
+  build_window(t);
+  build_mel(t);
+  build_twiddles(t);
+  build_post_twiddles(t);
+  build_fft_schedule(t);
+}
+
+}  // namespace catears

@@ -1,0 +1,283 @@
+"""ctypes binding of libcatears_hip.so (include/catears_gpu.h).
+
+This is the Python side of the drop-in boundary: the same C-ABI a C++ host
+(the reference's ce_stt.cc) links against.  Device memory and streams come
+from PyTorch (plumbing only); every compute call goes through the HIP library.
+There is no CPU fallback: if the library or a GPU is missing, calls raise.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libcatears_hip.so")
+
+CE_GPU_OK = 0
+ERRORS = {-2: "EINVAL", -3: "EHIP", -4: "EIO", -5: "ECORRUPT", -6: "ENOTSUP", -7: "ENOMEM"}
+
+# Every symbol include/catears_gpu.h declares (checked by tests).
+ABI = [
+    "ce_gpu_last_error", "ce_gpu_version", "ce_gpu_ctx_create", "ce_gpu_ctx_destroy",
+    "ce_gpu_ctx_set_stream", "ce_gpu_ctx_synchronize", "ce_gpu_ctx_profile",
+    "ce_gpu_ctx_profile_read", "ce_gpu_model_load_config",
+    "ce_gpu_model_load", "ce_gpu_model_info", "ce_gpu_model_tid2pdf", "ce_gpu_model_destroy",
+    "ce_gpu_fbank_num_frames", "ce_gpu_plan_create", "ce_gpu_plan_info",
+    "ce_gpu_plan_frame_offsets", "ce_gpu_plan_destroy", "ce_gpu_fbank", "ce_gpu_cmvn",
+    "ce_gpu_am_forward", "ce_gpu_score", "ce_gpu_sgemm", "ce_gpu_quantize",
+    "ce_gpu_gemm_u8u8f32", "ce_gpu_gemm_u8u8i32",
+]
+
+_lib = None
+
+
+class CatearsError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+def lib():
+    """Load the HIP library; raises ImportError if it was not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} missing: build it with `make` (hipcc, gfx950)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, ci, i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+    pp = ctypes.POINTER(ctypes.c_void_p)
+    pi, pi64 = ctypes.POINTER(ci), ctypes.POINTER(i64)
+    sig = {
+        "ce_gpu_last_error": (ctypes.c_char_p, []),
+        "ce_gpu_version": (ctypes.c_char_p, []),
+        "ce_gpu_ctx_create": (ci, [ci, vp, pp]),
+        "ce_gpu_ctx_destroy": (ci, [vp]),
+        "ce_gpu_ctx_set_stream": (ci, [vp, vp]),
+        "ce_gpu_ctx_synchronize": (ci, [vp]),
+        "ce_gpu_ctx_profile": (ci, [vp, ci]),
+        "ce_gpu_ctx_profile_read": (ci, [vp, ci, ctypes.POINTER(ctypes.c_double), pi64]),
+        "ce_gpu_model_load_config": (ci, [vp, ctypes.c_char_p, pp]),
+        "ce_gpu_model_load": (ci, [vp, ctypes.c_char_p, ctypes.c_char_p, ci, ci, pp]),
+        "ce_gpu_model_info": (ci, [vp, pi, pi, pi, pi, pi, pi64]),
+        "ce_gpu_model_tid2pdf": (ci, [vp, ctypes.POINTER(ctypes.c_int32), ci, pi]),
+        "ce_gpu_model_destroy": (ci, [vp]),
+        "ce_gpu_fbank_num_frames": (i64, [i64]),
+        "ce_gpu_plan_create": (ci, [vp, vp, pi64, ci, ci, pp]),
+        "ce_gpu_plan_info": (ci, [vp, pi, pi64, pi64, pi, pi]),
+        "ce_gpu_plan_frame_offsets": (ci, [vp, pi64]),
+        "ce_gpu_plan_destroy": (ci, [vp]),
+        "ce_gpu_fbank": (ci, [vp, vp, vp, vp, vp]),
+        "ce_gpu_cmvn": (ci, [vp, vp, vp, vp, vp]),
+        "ce_gpu_am_forward": (ci, [vp, vp, vp, vp, vp]),
+        "ce_gpu_score": (ci, [vp, vp, vp, vp, vp, vp, vp]),
+        "ce_gpu_sgemm": (ci, [vp, ci, ci, ci, vp, ci, vp, ci, vp, ci]),
+        "ce_gpu_quantize": (ci, [vp, vp, i64, vp, vp]),
+        "ce_gpu_gemm_u8u8f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp]),
+        "ce_gpu_gemm_u8u8i32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != CE_GPU_OK:
+        raise CatearsError(rc, lib().ce_gpu_last_error().decode())
+    return rc
+
+
+def _ptr(t):
+    """Device pointer of a torch tensor (or None)."""
+    if t is None:
+        return None
+    if not t.is_cuda or not t.is_contiguous():
+        raise ValueError("expected a contiguous device tensor")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+class Context:
+    """One device + one stream (defaults to torch's current stream)."""
+
+    def __init__(self, device=0, stream=None):
+        import torch
+        self.device = device
+        self._torch_stream = stream if stream is not None else torch.cuda.current_stream(device)
+        h = ctypes.c_void_p()
+        check(lib().ce_gpu_ctx_create(device, ctypes.c_void_p(self._torch_stream.cuda_stream),
+                                      ctypes.byref(h)))
+        self.h = h
+
+    def set_stream(self, stream):
+        self._torch_stream = stream
+        check(lib().ce_gpu_ctx_set_stream(self.h, ctypes.c_void_p(stream.cuda_stream)))
+
+    def synchronize(self):
+        check(lib().ce_gpu_ctx_synchronize(self.h))
+
+    PROF_GEMM, PROF_GEMM_GATHER, PROF_FBANK, PROF_CMVN, PROF_FINALIZE = range(5)
+
+    def profile(self, enable=True):
+        check(lib().ce_gpu_ctx_profile(self.h, int(enable)))
+
+    def profile_read(self, cls):
+        """(total_ms, launches) of a kernel class since the last read."""
+        ms, n = ctypes.c_double(), ctypes.c_int64()
+        check(lib().ce_gpu_ctx_profile_read(self.h, cls, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().ce_gpu_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Model:
+    def __init__(self, ctx, config_path=None, nnet=None, prior=None, left=None, right=None):
+        h = ctypes.c_void_p()
+        if config_path is not None:
+            check(lib().ce_gpu_model_load_config(ctx.h, config_path.encode(), ctypes.byref(h)))
+        else:
+            check(lib().ce_gpu_model_load(ctx.h, nnet.encode(), prior.encode(), left, right,
+                                          ctypes.byref(h)))
+        self.h = h
+        v = [ctypes.c_int() for _ in range(5)]
+        p = ctypes.c_int64()
+        check(lib().ce_gpu_model_info(h, *[ctypes.byref(x) for x in v], ctypes.byref(p)))
+        self.left, self.right, self.input_dim, self.num_pdfs, self.num_linear = [x.value for x in v]
+        self.num_params = p.value
+
+    def tid2pdf(self):
+        n = ctypes.c_int()
+        check(lib().ce_gpu_model_tid2pdf(self.h, None, 0, ctypes.byref(n)))
+        out = np.zeros(n.value, np.int32)
+        check(lib().ce_gpu_model_tid2pdf(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                         n.value, ctypes.byref(n)))
+        return out
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().ce_gpu_model_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def num_frames(n_samples):
+    return lib().ce_gpu_fbank_num_frames(int(n_samples))
+
+
+class Plan:
+    def __init__(self, ctx, num_samples, model=None, max_rows=4096):
+        ns = np.ascontiguousarray(num_samples, np.int64)
+        h = ctypes.c_void_p()
+        check(lib().ce_gpu_plan_create(ctx.h, model.h if model else None,
+                                       ns.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                       len(ns), max_rows, ctypes.byref(h)))
+        self.h = h
+        a, d, e = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        b, c = ctypes.c_int64(), ctypes.c_int64()
+        check(lib().ce_gpu_plan_info(h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c),
+                                     ctypes.byref(d), ctypes.byref(e)))
+        self.n_utt, self.total_samples, self.total_frames = a.value, b.value, c.value
+        self.n_chunks, self.max_chunk_rows = d.value, e.value
+        off = np.zeros(self.n_utt + 1, np.int64)
+        check(lib().ce_gpu_plan_frame_offsets(h, off.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
+        self.frame_offsets = off
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().ce_gpu_plan_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def fbank(ctx, plan, pcm, feats=None, mel=None):
+    import torch
+    if feats is None:
+        feats = torch.empty((plan.total_frames, 40), dtype=torch.float32, device=pcm.device)
+    check(lib().ce_gpu_fbank(ctx.h, plan.h, _ptr(pcm), _ptr(feats), _ptr(mel)))
+    return feats
+
+
+def cmvn(ctx, plan, global_stats, feats, out=None):
+    import torch
+    if out is None:
+        out = torch.empty_like(feats)
+    check(lib().ce_gpu_cmvn(ctx.h, plan.h, _ptr(global_stats), _ptr(feats), _ptr(out)))
+    return out
+
+
+def am_forward(ctx, model, plan, feats, out=None):
+    import torch
+    if out is None:
+        out = torch.empty((plan.total_frames, model.num_pdfs), dtype=torch.float32, device=feats.device)
+    check(lib().ce_gpu_am_forward(ctx.h, model.h, plan.h, _ptr(feats), _ptr(out)))
+    return out
+
+
+def score(ctx, model, plan, pcm, global_stats=None, ws=None, out=None):
+    import torch
+    if ws is None:
+        ws = torch.empty((2 * plan.total_frames * 40 + 1,), dtype=torch.float32, device=pcm.device)
+    if out is None:
+        out = torch.empty((plan.total_frames, model.num_pdfs), dtype=torch.float32, device=pcm.device)
+    check(lib().ce_gpu_score(ctx.h, model.h, plan.h, _ptr(pcm), _ptr(global_stats), _ptr(ws), _ptr(out)))
+    return out
+
+
+def sgemm(ctx, a, b, c=None):
+    import torch
+    m, k = a.shape
+    n = b.shape[1]
+    if c is None:
+        c = torch.empty((m, n), dtype=torch.float32, device=a.device)
+    check(lib().ce_gpu_sgemm(ctx.h, m, n, k, _ptr(a), a.stride(0), _ptr(b), b.stride(0), _ptr(c),
+                             c.stride(0)))
+    return c
+
+
+def quantize(ctx, x):
+    """Returns (uint8 tensor, 8-byte device params tensor {f32 scale, i32 zp})."""
+    import torch
+    q = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+    prm = torch.empty(2, dtype=torch.int32, device=x.device)
+    check(lib().ce_gpu_quantize(ctx.h, _ptr(x), x.numel(), _ptr(q), _ptr(prm)))
+    return q, prm
+
+
+def params_host(prm):
+    """(scale, zero_point) of a device params record."""
+    raw = prm.cpu().numpy()
+    return float(raw[:1].view(np.float32)[0]), int(raw[1])
+
+
+def gemm_u8(ctx, a, pa, b, pb, out_int32=False):
+    import torch
+    m, k = a.shape
+    n = b.shape[1]
+    if out_int32:
+        c = torch.empty((m, n), dtype=torch.int32, device=a.device)
+        check(lib().ce_gpu_gemm_u8u8i32(ctx.h, m, n, k, _ptr(a), _ptr(pa), _ptr(b), _ptr(pb), _ptr(c)))
+    else:
+        c = torch.empty((m, n), dtype=torch.float32, device=a.device)
+        check(lib().ce_gpu_gemm_u8u8f32(ctx.h, m, n, k, _ptr(a), _ptr(pa), _ptr(b), _ptr(pb), _ptr(c)))
+    return c

@@ -1,0 +1,204 @@
+/*
+ * catears_gpu.h -- C-ABI boundary of the MI355X acoustic-scoring path.
+ *
+ * The reference (ishine/CatEars, a.k.a. pocketkaldi) computes
+ *   PCM -> Fbank::Process -> CMVN::GetFrame -> AcousticModel::Process/EndOfStream
+ *       -> Nnet::Propagate -> (- log prior) -> log-likelihood rows
+ * on one CPU core, one frame at a time.  This header is the thin extern "C"
+ * FFI under which the same path runs as hand-written gfx950 HIP kernels, on
+ * whole utterances batched together.  Plain pointers, sizes and opaque
+ * handles only; every entry point returns an int status (CE_GPU_OK == 0) and
+ * never throws across the ABI.  The message of the last failure on the
+ * calling thread is returned by ce_gpu_last_error().
+ *
+ * Pointers named d_* are device (HBM) pointers; h_* are host pointers.  All
+ * device work is enqueued on the context's stream (asynchronous) unless a
+ * function says otherwise.
+ *
+ * Reference interfaces replaced (all paths relative to the reference root):
+ *   Fbank::Process            src/fbank.h:57-59,  src/fbank.cc:265-314
+ *   CMVN::CMVN / GetFrame     src/cmvn.h:22-26,   src/cmvn.cc:100-119
+ *   AcousticModel::Read       src/am.h:34-35,     src/am.cc:26-64
+ *   AcousticModel::Process /
+ *   EndOfStream / ComputeBatch src/am.h:41-47,    src/am.cc:82-164
+ *   Nnet::Read / Propagate    src/nnet.h:229-232, src/nnet.cc:273-307
+ *   MatMat (cblas_sgemm)      src/matrix.h:248-251, src/matrix.cc:300-323
+ *   Quantize                  src/matrix.h:238-240, src/matrix.cc:366-387
+ *   MatMat_U8U8F32            src/matrix.h:254-260, src/matrix.cc:389-420
+ *   ce_stt_last_error         src/ce_stt.h:74-76 (per-thread here, not global)
+ */
+#ifndef CATEARS_GPU_H_
+#define CATEARS_GPU_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CE_GPU_OK 0
+#define CE_GPU_EINVAL (-2)    /* bad argument / shape (reference: assert)        */
+#define CE_GPU_EHIP (-3)      /* HIP runtime error                                */
+#define CE_GPU_EIO (-4)       /* cannot open / read a file (Status::IOError)      */
+#define CE_GPU_ECORRUPT (-5)  /* malformed model/config (Status::Corruption)      */
+#define CE_GPU_ENOTSUP (-6)   /* model topology this path does not run            */
+#define CE_GPU_ENOMEM (-7)    /* device allocation failed (std::bad_alloc)        */
+
+/* Feature geometry fixed at compile time in the reference (src/fbank.h:7-13). */
+#define CE_GPU_FBANK_DIM 40
+#define CE_GPU_FRAME_SHIFT 160
+#define CE_GPU_FRAME_LENGTH 400
+
+typedef struct ce_gpu_ctx ce_gpu_ctx;     /* device + stream + workspaces + fbank tables */
+typedef struct ce_gpu_model ce_gpu_model; /* device-resident nnet, log prior, contexts   */
+typedef struct ce_gpu_plan ce_gpu_plan;   /* geometry of one batch of utterances         */
+
+/* Message of the last failure on this thread ("" if none). */
+const char *ce_gpu_last_error(void);
+
+/* Library version string. */
+const char *ce_gpu_version(void);
+
+/* ------------------------------------------------------------ context --- */
+
+/* Create a context on `device` that enqueues on `stream` (a hipStream_t; NULL
+ * = the legacy default stream).  Builds the fbank tables on the host with the
+ * reference's formulas (Hamming window src/fbank.cc:248-255, mel banks
+ * src/fbank.cc:103-163, split-radix tables src/srfft.cc:74-122) and uploads
+ * them once. */
+int ce_gpu_ctx_create(int device, void *stream, ce_gpu_ctx **out);
+int ce_gpu_ctx_destroy(ce_gpu_ctx *ctx);
+int ce_gpu_ctx_set_stream(ce_gpu_ctx *ctx, void *stream);
+/* Block the host until all work enqueued through ctx has finished. */
+int ce_gpu_ctx_synchronize(ce_gpu_ctx *ctx);
+
+/* Kernel timing for roofline reporting: while enabled, every launch of the
+ * given kernel class is bracketed by a pair of HIP events on the context's
+ * stream.  ce_gpu_ctx_profile_read synchronizes, returns the summed event
+ * durations (ms) and launch count of the class since it was enabled, and
+ * resets them.  Classes: 0 = TDNN GEMM, A operand in 16-byte vectors
+ * (layers whose input width is a multiple of 32); 1 = TDNN GEMM, gathered A
+ * (first layer); 2 = fbank; 3 = CMVN; 4 = log-softmax/prior finalize. */
+#define CE_GPU_PROF_GEMM 0
+#define CE_GPU_PROF_GEMM_GATHER 1
+#define CE_GPU_PROF_FBANK 2
+#define CE_GPU_PROF_CMVN 3
+#define CE_GPU_PROF_FINALIZE 4
+#define CE_GPU_PROF_CLASSES 5
+int ce_gpu_ctx_profile(ce_gpu_ctx *ctx, int enable);
+int ce_gpu_ctx_profile_read(ce_gpu_ctx *ctx, int kernel_class, double *total_ms, int64_t *launches);
+
+/* -------------------------------------------------------------- model --- */
+
+/* AcousticModel::Read (src/am.cc:26-64): reads the key=value config (keys
+ * nnet, prior, left_context, right_context, chunk_size, num_pdfs, tid2pdf;
+ * relative paths resolved against the config's directory,
+ * src/configuration.cc:52-66), the NN02 nnet (src/nnet.cc:221-293), the VEC0
+ * prior (then log, src/am.cc:41-44) and the tid2pdf map; uploads weights.
+ * Fails with CE_GPU_ENOTSUP for a topology whose whole-utterance result
+ * would differ from the reference's chunked one. */
+int ce_gpu_model_load_config(ce_gpu_ctx *ctx, const char *config_path, ce_gpu_model **out);
+
+/* The same from explicit files; left/right context as AcousticModel reads
+ * them from its config (src/am.cc:48-50). */
+int ce_gpu_model_load(ce_gpu_ctx *ctx, const char *nnet_path, const char *prior_path,
+                      int left_context, int right_context, ce_gpu_model **out);
+
+/* Shape of a loaded model.  Any output pointer may be NULL. */
+int ce_gpu_model_info(const ce_gpu_model *m, int *left_context, int *right_context,
+                      int *input_dim, int *num_pdfs, int *num_linear, int64_t *num_params);
+
+/* tid2pdf map (AcousticModel::TransitionPdfIdMap, src/am.h:38-40).  Copies
+ * min(capacity, size) ints to h_out and returns the size via *size. */
+int ce_gpu_model_tid2pdf(const ce_gpu_model *m, int32_t *h_out, int capacity, int *size);
+int ce_gpu_model_destroy(ce_gpu_model *m);
+
+/* --------------------------------------------------------------- plan --- */
+
+/* Frames of one utterance of n samples: 0 if n < 400 else 1 + (n - 400) / 160
+ * (src/fbank.cc:35-42, snip-edges). */
+int64_t ce_gpu_fbank_num_frames(int64_t num_samples);
+
+/* Describe a batch of n_utt utterances laid out back to back in one PCM
+ * buffer (utterance u starts at sample sum_{v<u} h_num_samples[v]).  Frames
+ * and log-likelihood rows are laid out the same way (utterance u's rows start
+ * at sum_{v<u} T_v).  If `model` is non-NULL the plan also packs the
+ * utterances into nnet chunks of at most `max_rows` rows each (T_u + L + R
+ * rows per utterance; longer utterances are split into segments that overlap
+ * by L + R input rows, which the reference shows gives identical rows,
+ * src/am.cc:73-80).  max_rows <= 0 selects 4096. */
+int ce_gpu_plan_create(ce_gpu_ctx *ctx, const ce_gpu_model *model, const int64_t *h_num_samples,
+                       int n_utt, int max_rows, ce_gpu_plan **out);
+/* Totals of a plan; any output may be NULL. */
+int ce_gpu_plan_info(const ce_gpu_plan *p, int *n_utt, int64_t *total_samples,
+                     int64_t *total_frames, int *n_chunks, int *max_chunk_rows);
+/* Per-utterance frame (= log-likelihood row) offsets, n_utt + 1 entries. */
+int ce_gpu_plan_frame_offsets(const ce_gpu_plan *p, int64_t *h_out);
+int ce_gpu_plan_destroy(ce_gpu_plan *p);
+
+/* ------------------------------------------------------------ compute --- */
+
+/* Fbank::Process over every utterance of the plan (one-shot, equivalent to
+ * streaming, src/fbank.cc:265-314): d_pcm holds total_samples floats at raw
+ * int16 scale (src/pcm_reader.cc:174); d_feats receives total_frames x 40
+ * log-mel energies.  If d_mel is non-NULL the pre-log mel energies (same
+ * shape) are written too (debug / parity). */
+int ce_gpu_fbank(ce_gpu_ctx *ctx, const ce_gpu_plan *p, const float *d_pcm, float *d_feats,
+                 float *d_mel);
+
+/* Online CMVN (src/cmvn.cc:35-110) over every utterance: d_global_stats is
+ * the 41-float VEC0 payload (40 sums + count); frames are processed in order
+ * per utterance exactly like GetFrame(0), GetFrame(1), ...  d_out must not
+ * overlap d_feats (the window subtracts frames read 600 steps earlier). */
+int ce_gpu_cmvn(ce_gpu_ctx *ctx, const ce_gpu_plan *p, const float *d_global_stats,
+                const float *d_feats, float *d_out);
+
+/* AcousticModel::Process* + EndOfStream for every utterance of the plan:
+ * d_feats is total_frames x input_dim; d_loglik receives total_frames x
+ * num_pdfs rows of nnet output minus log prior (src/am.cc:104-112). */
+int ce_gpu_am_forward(ce_gpu_ctx *ctx, const ce_gpu_model *m, const ce_gpu_plan *p,
+                      const float *d_feats, float *d_loglik);
+
+/* The whole path: fbank -> (CMVN if d_global_stats != NULL) -> nnet -> - log
+ * prior.  d_feats_ws must hold 2 x total_frames x 40 floats (features and
+ * normalised features). */
+int ce_gpu_score(ce_gpu_ctx *ctx, const ce_gpu_model *m, const ce_gpu_plan *p,
+                 const float *d_pcm, const float *d_global_stats, float *d_feats_ws,
+                 float *d_loglik);
+
+/* ------------------------------------------------------- linear algebra --- */
+
+/* MatMat (src/matrix.cc:300-323): C[m x n] = A[m x k] * B[k x n], all
+ * row-major with leading dimensions lda/ldb/ldc (in floats), fp32 in, fp32
+ * MFMA accumulate. */
+int ce_gpu_sgemm(ce_gpu_ctx *ctx, int m, int n, int k, const float *d_a, int lda,
+                 const float *d_b, int ldb, float *d_c, int ldc);
+
+/* Quantize (src/matrix.cc:329-387): per-tensor asymmetric uint8 with the
+ * reference's min/max (max initialised to FLT_MIN), scale = (max-min)/255
+ * (double, stored float), zero point = round(-min/scale) unclamped.  d_q
+ * receives count bytes; the parameters are written to d_params as
+ * {float scale, int32 zero_point} (device, 8 bytes) so the call stays
+ * asynchronous. */
+int ce_gpu_quantize(ce_gpu_ctx *ctx, const float *d_x, int64_t count, uint8_t *d_q,
+                    void *d_params);
+
+/* MatMat_U8U8F32 (src/matrix.cc:389-420 -> gemmlowp EightBitIntGemm):
+ * C[m x n] = float(int32 sum_k (A-zpA)(B-zpB)) * (sA*sB), A m x k and B k x n
+ * row-major uint8, parameters read from the device records written by
+ * ce_gpu_quantize.  The int32 accumulator is bit-exact. */
+int ce_gpu_gemm_u8u8f32(ce_gpu_ctx *ctx, int m, int n, int k, const uint8_t *d_a,
+                        const void *d_params_a, const uint8_t *d_b, const void *d_params_b,
+                        float *d_c);
+
+/* The same, int32 accumulators out (no scaling): the quantity gemmlowp's
+ * GemmWithOutputPipeline produces before the float stage. */
+int ce_gpu_gemm_u8u8i32(ce_gpu_ctx *ctx, int m, int n, int k, const uint8_t *d_a,
+                        const void *d_params_a, const uint8_t *d_b, const void *d_params_b,
+                        int32_t *d_c);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+#endif
+
+#endif /* CATEARS_GPU_H_ */

@@ -1,0 +1,253 @@
+"""Parity of the HIP path (through the C-ABI) with the oracle, on an MI355X.
+
+Bars: bit-exact where the reference is exact IEEE arithmetic -- pre-log mel
+energies, CMVN, Quantize, the int32 u8 GEMM accumulator -- and for fp32 GEMM
+work the north-star tolerance, |loglik - oracle| <= 1e-4 absolute.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+LOGLIK_TOL = 1e-4   # BASELINE.json north star: log-likelihoods within 1e-4
+FEAT_TOL = 1e-5     # log-mel: only the final logf may differ (<= 1-2 ulp)
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return torch
+
+
+@pytest.fixture(scope="module")
+def G():
+    from catears_amd import gpu
+    gpu.lib()  # fail loudly if the HIP library is missing
+    return gpu
+
+
+@pytest.fixture(scope="module")
+def ctx(torch, G):
+    return G.Context(0)
+
+
+def dev(torch, x):
+    return torch.from_numpy(np.ascontiguousarray(x)).cuda()
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def gpu_fbank(torch, G, ctx, waves, with_mel=True):
+    plan = G.Plan(ctx, [len(w) for w in waves])
+    pcm = dev(torch, np.concatenate(waves) if waves else np.zeros(1, np.float32))
+    feats = torch.empty((max(plan.total_frames, 1), 40), dtype=torch.float32, device="cuda")
+    mel = torch.empty_like(feats) if with_mel else None
+    G.fbank(ctx, plan, pcm, feats, mel)
+    torch.cuda.synchronize()
+    off = plan.frame_offsets
+    f = feats.cpu().numpy()[:plan.total_frames]
+    m = mel.cpu().numpy()[:plan.total_frames] if with_mel else None
+    return plan, off, f, m
+
+
+# ------------------------------------------------------------------ fbank --
+
+def test_fbank_goldens(torch, G, ctx, oracle):
+    waves = [oracle.read_wav(os.path.join(GOLDEN, n)) for n in ("en-us-hello.wav", "en-us-cat.wav")]
+    plan, off, f, m = gpu_fbank(torch, G, ctx, waves)
+    fb = oracle.Fbank()
+    for u, w in enumerate(waves):
+        of, om = fb.compute(w, with_mel=True)
+        assert np.array_equal(bits(m[off[u]:off[u + 1]]), bits(om)), "pre-log mel not bit-exact"
+        assert np.abs(f[off[u]:off[u + 1]] - of).max() <= FEAT_TOL
+    k = np.loadtxt(os.path.join(GOLDEN, "fbankmat_en-us-hello.wav.txt")).reshape(-1, 40)
+    assert np.abs(f[:47] - k).max() < 1e-4  # test/fbank_test.cc:56
+
+
+def test_fbank_ragged_batch_edges(torch, G, ctx, oracle):
+    from catears_amd import synth
+    lengths = [0, 399, 400, 559, 560, 16000, 160000, 1, 1600000]
+    waves = [synth.pcm(100 + i, n) for i, n in enumerate(lengths)]
+    waves.append(np.zeros(16000, np.float32))                 # log-floor path
+    waves.append(np.full(16000, 32767.0, np.float32))         # DC only
+    plan, off, f, m = gpu_fbank(torch, G, ctx, waves)
+    fb = oracle.Fbank()
+    for u, w in enumerate(waves):
+        of, om = fb.compute(w, with_mel=True)
+        assert off[u + 1] - off[u] == len(of)
+        if len(of):
+            assert np.array_equal(bits(m[off[u]:off[u + 1]]), bits(om)), f"utt {u}"
+            assert np.abs(f[off[u]:off[u + 1]] - of).max() <= FEAT_TOL
+
+
+# ------------------------------------------------------------------- cmvn --
+
+def test_cmvn_bitexact(torch, G, ctx, oracle, global_stats):
+    from catears_amd import synth
+    waves = [synth.pcm(200 + i, n) for i, n in enumerate([16000, 400, 0, 160000, 250000])]
+    plan, off, f, _ = gpu_fbank(torch, G, ctx, waves, with_mel=False)
+    feats = dev(torch, f)
+    out = G.cmvn(ctx, plan, dev(torch, global_stats), feats)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    for u in range(len(waves)):
+        ref = oracle.cmvn(global_stats, f[off[u]:off[u + 1]])
+        assert np.array_equal(bits(o[off[u]:off[u + 1]]), bits(ref)), f"utt {u}"
+    k = np.loadtxt(os.path.join(GOLDEN, "fbankcmvnmat_en-us-hello.wav.txt")).reshape(-1, 40)
+    w = oracle.read_wav(os.path.join(GOLDEN, "en-us-hello.wav"))
+    p2, _, f2, _ = gpu_fbank(torch, G, ctx, [w], with_mel=False)
+    c2 = G.cmvn(ctx, p2, dev(torch, global_stats), dev(torch, f2)).cpu().numpy()
+    assert np.abs(c2 - k).max() < 1e-4  # test/cmvn_test.cc:76, two-sided
+
+
+def test_cmvn_rejects_aliasing(torch, G, ctx, global_stats):
+    plan = G.Plan(ctx, [16000])
+    x = torch.zeros((plan.total_frames, 40), dtype=torch.float32, device="cuda")
+    with pytest.raises(G.CatearsError):
+        G.cmvn(ctx, plan, dev(torch, global_stats), x, x)
+
+
+# --------------------------------------------------------------------- am --
+
+def am_oracle(oracle, am, feats, gemm=None):
+    return oracle.am_stream(am, feats, chunk_size=am["chunk"], gemm=gemm)
+
+
+def test_am_xs_vs_oracle(torch, G, ctx, oracle, xs_config):
+    from catears_amd import formats, synth
+    am = formats.read_am(xs_config)
+    model = G.Model(ctx, xs_config)
+    assert (model.left, model.right, model.input_dim, model.num_pdfs) == (10, 10, 40, 512)
+    assert np.array_equal(model.tid2pdf(), am["tid2pdf"])
+    fb = oracle.Fbank()
+    feats = [fb.compute(synth.pcm(300 + i, n)) for i, n in enumerate([16000, 560, 400, 48000, 3000])]
+    feats.insert(2, np.zeros((0, 40), np.float32))
+    plan = G.Plan(ctx, [(len(x) - 1) * 160 + 400 if len(x) else 0 for x in feats], model)
+    assert plan.total_frames == sum(len(x) for x in feats)
+    out = G.am_forward(ctx, model, plan, dev(torch, np.concatenate(feats)))
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    off = plan.frame_offsets
+    for u, x in enumerate(feats):
+        ref = am_oracle(oracle, am, x)
+        assert ref.shape == (off[u + 1] - off[u], 512)
+        if len(x):
+            assert np.abs(o[off[u]:off[u + 1]] - ref).max() <= LOGLIK_TOL, f"utt {u}"
+
+
+def test_am_segmentation_is_exact(torch, G, ctx, oracle, xs_config):
+    """Splitting an utterance over chunks (max_rows) must not change a bit:
+    every output element is the same k-ordered MFMA chain whatever the row's
+    position."""
+    from catears_amd import synth
+    model = G.Model(ctx, xs_config)
+    fb = oracle.Fbank()
+    feats = [fb.compute(synth.pcm(400 + i, n)) for i, n in enumerate([48000, 16000, 30000])]
+    ns = [(len(x) - 1) * 160 + 400 for x in feats]
+    x = dev(torch, np.concatenate(feats))
+    outs = []
+    for max_rows in (4096, 333, 64):
+        plan = G.Plan(ctx, ns, model, max_rows=max_rows)
+        outs.append(G.am_forward(ctx, model, plan, x).cpu().numpy())
+    assert np.array_equal(bits(outs[0]), bits(outs[1]))
+    assert np.array_equal(bits(outs[0]), bits(outs[2]))
+
+
+def test_am_s_vs_oracle(torch, G, ctx, oracle, s_config):
+    """Benchmark model (TDNN-S, 34.75 MFLOP/frame) on two utterances; the
+    oracle's GEMM is numpy fp32 here for speed (any fp32 summation order is
+    the reference algorithm; OpenBLAS's order is not pinned either)."""
+    from catears_amd import formats, synth
+    am = formats.read_am(s_config)
+    model = G.Model(ctx, s_config)
+    assert model.num_pdfs == 3456 and model.num_linear == 7
+    fb = oracle.Fbank()
+    feats = [fb.compute(synth.pcm(500 + i, n)) for i, n in enumerate([48000, 20000])]
+    plan = G.Plan(ctx, [48000, 20000], model)
+    out = G.am_forward(ctx, model, plan, dev(torch, np.concatenate(feats))).cpu().numpy()
+    off = plan.frame_offsets
+    for u, x in enumerate(feats):
+        ref = oracle.am_whole(am, x, gemm=lambda a, w: a @ w)
+        assert np.abs(out[off[u]:off[u + 1]] - ref).max() <= LOGLIK_TOL
+
+
+def test_score_pipeline_with_cmvn(torch, G, ctx, oracle, xs_config, global_stats):
+    from catears_amd import formats, synth
+    am = formats.read_am(xs_config)
+    model = G.Model(ctx, xs_config)
+    waves = [synth.pcm(600 + i, n) for i, n in enumerate([32000, 16000, 799])]
+    plan = G.Plan(ctx, [len(w) for w in waves], model)
+    out = G.score(ctx, model, plan, dev(torch, np.concatenate(waves)), dev(torch, global_stats)).cpu().numpy()
+    off = plan.frame_offsets
+    fb = oracle.Fbank()
+    for u, w in enumerate(waves):
+        ref = am_oracle(oracle, am, oracle.cmvn(global_stats, fb.compute(w)))
+        assert np.abs(out[off[u]:off[u + 1]] - ref).max() <= LOGLIK_TOL
+
+
+def test_model_rejects_bad_topology(torch, G, ctx, tmp_path):
+    from catears_amd import formats
+    W = np.ones((40, 8), np.float32)
+    layers = [{"kind": "splice", "indices": [-1, 0, 1]}, {"kind": "linear", "W": np.ones((120, 8), np.float32),
+                                                          "b": np.zeros(8, np.float32)}]
+    p = tmp_path / "bad.nnet"
+    p.write_bytes(formats.nnet_bytes(layers, 1, 1))
+    pr = tmp_path / "bad.prior"
+    pr.write_bytes(formats.vec_bytes(np.full(8, 0.125, np.float32)))
+    with pytest.raises(G.CatearsError) as e:
+        G.Model(ctx, nnet=str(p), prior=str(pr), left=1, right=1)
+    assert e.value.code == -6  # ENOTSUP: splice without its narrow
+    p.write_bytes(b"NN02" + b"\x00" * 8 + (1).to_bytes(4, "little") + b"LAY0" + (5).to_bytes(4, "little"))
+    with pytest.raises(G.CatearsError) as e:
+        G.Model(ctx, nnet=str(p), prior=str(pr), left=0, right=0)
+    assert e.value.code == -5 and "unexpected layer type" in str(e.value)
+    del W
+
+
+# ------------------------------------------------------------ linear alg --
+
+@pytest.mark.parametrize("shape", [(5, 3, 2), (100, 100, 1), (1024, 1024, 80), (121, 233, 17),
+                                   (4096, 1024, 3072), (300, 3456, 1024)])
+def test_sgemm(torch, G, ctx, shape):
+    m, n, k = shape
+    rng = np.random.default_rng(m + n + k)
+    A = rng.uniform(-0.5, 0.5, (m, k)).astype(np.float32)
+    B = rng.uniform(1, 2, (k, n)).astype(np.float32)
+    C = G.sgemm(ctx, dev(torch, A), dev(torch, B)).cpu().numpy()
+    exact = A.astype(np.float64) @ B.astype(np.float64)
+    # fp32 fma chain: error << test/gemm_test.cc:104's 1e-2
+    assert np.abs(C - exact).max() <= 1e-6 * np.abs(A).sum(1).max() * 2 * k ** 0.5 + 1e-5
+
+
+@pytest.mark.parametrize("shape", [(5, 3, 2), (100, 100, 1), (1024, 1024, 80), (121, 233, 17),
+                                   (257, 300, 1000), (8192, 1024, 3072)])
+def test_quantize_and_u8_gemm_bitexact(torch, G, ctx, oracle, shape):
+    m, n, k = shape
+    rng = np.random.default_rng(3 * m + n)
+    A = rng.uniform(-0.5, 0.5, (m, k)).astype(np.float32)
+    B = rng.uniform(1, 2, (k, n)).astype(np.float32)
+    qa, pa = G.quantize(ctx, dev(torch, A))
+    qb, pb = G.quantize(ctx, dev(torch, B))
+    oa, sa, za = oracle.quantize(A)
+    ob, sb, zb = oracle.quantize(B)
+    assert G.params_host(pa) == (sa, za) and G.params_host(pb) == (sb, zb)
+    assert np.array_equal(qa.cpu().numpy(), oa) and np.array_equal(qb.cpu().numpy(), ob)
+    if m * n * k > 2e9:  # oracle int32 GEMM too slow: check a row/column sample
+        ri = rng.choice(m, 16, replace=False)
+        ci = np.arange(n)
+        ref_i = oracle.gemm_u8u8_i32(oa[ri], za, ob, zb)
+        got_i = G.gemm_u8(ctx, qa, pa, qb, pb, out_int32=True).cpu().numpy()[ri][:, ci]
+        assert np.array_equal(got_i, ref_i)
+        return
+    ref_i = oracle.gemm_u8u8_i32(oa, za, ob, zb)
+    got_i = G.gemm_u8(ctx, qa, pa, qb, pb, out_int32=True).cpu().numpy()
+    assert np.array_equal(got_i, ref_i)
+    got_f = G.gemm_u8(ctx, qa, pa, qb, pb).cpu().numpy()
+    assert np.array_equal(bits(got_f), bits(oracle.gemm_u8u8f32(oa, sa, za, ob, sb, zb)))
