@@ -13,7 +13,9 @@ LIB := catears_amd/lib/libcatears_hip.so
 # epilogue arithmetic bit-identical to it.  MFMA accumulation is unaffected.
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off \
             -Iinclude -I$(SRC) -Wall -Wno-unused-function
-HOSTFLAGS := -O2 -fPIC -std=c++17 -ffp-contract=off -Iinclude -I$(SRC) -Wall
+CXX ?= g++
+HOSTFLAGS := -O2 -fPIC -std=c++17 -ffp-contract=off -Iinclude -I$(SRC) -I/opt/rocm/include \
+             -D__HIP_PLATFORM_AMD__ -Wall
 
 KERNELS := $(wildcard $(SRC)/kernels/*.hip)
 HOSTSRC := $(SRC)/capi.cc $(SRC)/tables.cc
@@ -29,7 +31,7 @@ $(OBJ)/%.o: $(SRC)/kernels/%.hip $(HDRS)
 
 $(OBJ)/%.o: $(SRC)/%.cc $(HDRS)
 	@mkdir -p $(OBJ)
-	$(HIPCC) $(HOSTFLAGS) -D__HIP_PLATFORM_AMD__ -c $< -o $@
+	$(CXX) $(HOSTFLAGS) -c $< -o $@
 
 $(LIB): $(OBJS)
 	@mkdir -p $(dir $(LIB))

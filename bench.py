@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--cpu-utts", type=int, default=32, help="utterances in the CPU baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the HIP-event kernel timing")
+    ap.add_argument("--serial", action="store_true", help="one stream: no front/back stage overlap")
     return ap.parse_args()
 
 
@@ -111,8 +112,13 @@ def main():
         dist.barrier()
     conf = synth.write_model(mdir, args.model)  # no-op once written
 
-    stream = torch.cuda.current_stream()
-    ctx = gpu.Context(local, stream)
+    # Two-stage software pipeline on two HIP streams: the front stage (fbank +
+    # CMVN, a handful of waves) of batch i+1 runs beside the nnet GEMMs of
+    # batch i.  Each batch is still scored end to end inside the timed region.
+    back = torch.cuda.current_stream()
+    front = torch.cuda.Stream() if not args.serial else back
+    ctx = gpu.Context(local, back)
+    ctx_f = gpu.Context(local, front) if not args.serial else ctx
     model = gpu.Model(ctx, conf)
     n_samp = int(16000 * args.seconds)
     U = args.utts_per_step
@@ -124,7 +130,10 @@ def main():
     pool = max(args.pool, U)
     pcm = torch.from_numpy(np.stack([synth.pcm(rank * 100003 + i, n_samp) for i in range(pool)])).cuda()
     gstats = None if args.no_cmvn else torch.from_numpy(synth.cmvn_stats_synthetic()).cuda()
-    ws = torch.empty(2 * frames_per_step * 40 + 1, dtype=torch.float32, device="cuda")
+    raw = [torch.empty((frames_per_step, 40), dtype=torch.float32, device="cuda") for _ in range(2)]
+    norm = [torch.empty_like(raw[0]) for _ in range(2)] if gstats is not None else raw
+    ready = [torch.cuda.Event() for _ in range(2)]
+    free = [torch.cuda.Event() for _ in range(2)]
     nbuf = 3
     outs = [torch.empty((frames_per_step, model.num_pdfs), dtype=torch.float32, device="cuda")
             for _ in range(nbuf)]
@@ -135,20 +144,35 @@ def main():
     pending = [None] * nbuf
     checksum = torch.zeros((), dtype=torch.float64, device="cuda")
 
-    def step(i):
-        slot = i % nbuf
-        if pending[slot] is not None:
-            pending[slot].wait()  # gather from nbuf steps ago has read this buffer
-            pending[slot] = None
+    def front_stage(i):
+        slot = i % 2
+        front.wait_event(free[slot])  # batch i-2 has finished reading this slot
         first = (i * U) % (pool - U + 1)
         src = pcm[first:first + U].reshape(-1)
-        gpu.score(ctx, model, plan, src, gstats, ws, outs[slot])
-        if gather:
-            pending[slot] = dist.gather(outs[slot], recv[slot] if rank == 0 else None, dst=0,
-                                        async_op=True)
+        gpu.fbank(ctx_f, plan, src, raw[slot])
+        if gstats is not None:
+            gpu.cmvn(ctx_f, plan, gstats, raw[slot], norm[slot])
+        ready[slot].record(front)
 
-    for i in range(args.warmup):
-        step(i)
+    def back_stage(i):
+        slot, o = i % 2, i % nbuf
+        if pending[o] is not None:
+            pending[o].wait()  # gather from nbuf steps ago has read this buffer
+            pending[o] = None
+        back.wait_event(ready[slot])
+        gpu.am_forward(ctx, model, plan, norm[slot], outs[o])
+        free[slot].record(back)
+        if gather:
+            pending[o] = dist.gather(outs[o], recv[o] if rank == 0 else None, dst=0, async_op=True)
+
+    def run(first, count):
+        front_stage(first)
+        for i in range(first, first + count):
+            if i + 1 < first + count:
+                front_stage(i + 1)
+            back_stage(i)
+
+    run(0, args.warmup)
     for w in pending:
         if w is not None:
             w.wait()
@@ -156,12 +180,12 @@ def main():
     torch.cuda.synchronize()
     if not args.no_profile:
         ctx.profile(True)
+        ctx_f.profile(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i)
+    run(args.warmup, args.steps)
     for w in pending:
         if w is not None:
             w.wait()
@@ -178,9 +202,11 @@ def main():
     prof = {}
     if not args.no_profile:
         ctx.profile(False)
-        for name, cls in (("gemm", ctx.PROF_GEMM), ("gemm_gather", ctx.PROF_GEMM_GATHER),
-                          ("fbank", ctx.PROF_FBANK), ("cmvn", ctx.PROF_CMVN), ("finalize", ctx.PROF_FINALIZE)):
-            prof[name] = ctx.profile_read(cls)
+        ctx_f.profile(False)
+        for name, c, cls in (("gemm", ctx, ctx.PROF_GEMM), ("gemm_gather", ctx, ctx.PROF_GEMM_GATHER),
+                             ("fbank", ctx_f, ctx.PROF_FBANK), ("cmvn", ctx_f, ctx.PROF_CMVN),
+                             ("finalize", ctx, ctx.PROF_FINALIZE)):
+            prof[name] = c.profile_read(cls)
 
     total_frames = frames_per_step * args.steps * world
     value = total_frames / elapsed
@@ -230,6 +256,7 @@ def main():
                                ("" if not gather else "; C4 RCCL gather of log-likelihoods to rank 0"),
                    "frames_per_step_per_gpu": frames_per_step, "packed_rows": plan.max_chunk_rows,
                    "cmvn": not args.no_cmvn, "parallelism": f"utterance shard x{world}",
+                   "streams": 1 if args.serial else 2,
                    "gather": gather},
         "roofline": roofline, "cpu_baseline": cpu, "stages": stages,
         "end_to_end_mfma_frac": round(value / world * FLOPS_PER_FRAME / 1e12 / MFMA_F32_PEAK_TFLOPS, 4),

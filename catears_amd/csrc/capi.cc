@@ -304,7 +304,7 @@ static int build_program(const std::vector<RawLayer> &layers, int left, int righ
           return fail(CE_GPU_ECORRUPT, fmt("Corruption: layer %zu expects width %d, got %d", i, g.din, width));
         if (m->steps.empty()) m->input_dim = g.din;
         g.k = in;
-        g.kpad = (in + 31) / 32 * 32;
+        g.kpad = (in + gemm_k_align() - 1) / gemm_k_align() * gemm_k_align();
         g.n = out;
         std::vector<float> wt((size_t)out * g.kpad, 0.0f);  // transpose to n x kpad
         for (int k = 0; k < in; ++k)
@@ -799,7 +799,7 @@ int ce_gpu_sgemm(ce_gpu_ctx *ctx, int m, int n, int k, const float *d_a, int lda
   a.m = m;
   a.n = n;
   a.k = k;
-  a.kpad = (k + 31) / 32 * 32;
+  a.kpad = (k + gemm_k_align() - 1) / gemm_k_align() * gemm_k_align();
   a.din = k;
   a.nseg = 1;
   a.w = d_b;

@@ -210,6 +210,8 @@ struct GemmArgs {
   int ldy = 0;
 };
 int launch_gemm_f32(hipStream_t s, const GemmArgs &a);
+// Weights' K dimension is zero-padded to a multiple of this (every tile variant's BK).
+int gemm_k_align();
 
 // Final step: optional log-softmax per row, minus log prior, scatter to the
 // output rows named by row_dst (-1 = drop).

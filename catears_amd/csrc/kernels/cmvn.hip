@@ -20,45 +20,72 @@ namespace {
 constexpr int kWindow = 600;  // PK_ONLINECMVN_WINDOW, src/cmvn.h:10
 constexpr int kGlobal = 200;  // PK_ONLINECMVN_GLOBALFRAMES, src/cmvn.h:11
 
+constexpr int kTile = 32;  // frames prefetched into registers per step of the chain
+
+// Everything in SmoothStats/Apply except the per-dimension sums depends only
+// on the frame index t (count = min(t+1, 600)) and on N_g, so it is computed
+// once per block into LDS: alpha_t (the float scalar of AddVec, cmvn.cc:80-88)
+// and neg_t = -(float)(1 / smoothed count) (cmvn.cc:93-97).  For t >= 600 no
+// smoothing happens and the count is exactly 600.
 __global__ __launch_bounds__(64) void cmvn_kernel(const int64_t *__restrict__ frame_off,
                                                   const float *__restrict__ gstats,
                                                   const float *__restrict__ in,
                                                   float *__restrict__ out) {
+  __shared__ float s_alpha[kWindow], s_neg[kWindow + 1];
   const int u = blockIdx.x, d = threadIdx.x;
+  const float g_count = gstats[kMel];
+  for (int t = d; t <= kWindow; t += 64) {
+    float count = (float)(t + 1 < kWindow ? t + 1 : kWindow);
+    float alpha = 0.0f;
+    if ((double)count < kWindow) {  // SmoothStats (cmvn.cc:70-89)
+      double from_global = kWindow - (double)count;
+      if (from_global > kGlobal) from_global = kGlobal;
+      alpha = (float)(from_global / (double)g_count);
+      count = alpha != 1.0f ? count + alpha * g_count : count + g_count;
+    }
+    if (t < kWindow) s_alpha[t] = alpha;
+    s_neg[t] = -(float)(1 / (double)count);  // Apply (cmvn.cc:91-98)
+  }
+  __syncthreads();
   if (d >= kMel) return;
   const int64_t r0 = frame_off[u];
   const int t_frames = (int)(frame_off[u + 1] - r0);
   const float g = gstats[d];
-  const float g_count = gstats[kMel];
   const float *x = in + r0 * kMel + d;
   float *y = out + r0 * kMel + d;
+  float cur[kTile], old[kTile], ncur[kTile], nold[kTile];
+  auto fetch = [&](int t0, float *c, float *o) {
+#pragma unroll
+    for (int i = 0; i < kTile; ++i) {
+      const int t = t0 + i;
+      c[i] = t < t_frames ? x[(int64_t)t * kMel] : 0.0f;
+      o[i] = (t >= kWindow && t < t_frames) ? x[(int64_t)(t - kWindow) * kMel] : 0.0f;
+    }
+  };
+  fetch(0, cur, old);
   float carry = 0.0f;
-#pragma unroll 4
-  for (int t = 0; t < t_frames; ++t) {
-    const float xt = x[(int64_t)t * kMel];
-    // ComputeStats: double temp seeded from the float carry
-    double acc = t > 0 ? (double)carry : 0.0;
-    acc += (double)xt;
-    float count = (float)(t + 1 < kWindow ? t + 1 : kWindow);
-    if (t >= kWindow) acc += -1.0 * (double)x[(int64_t)(t - kWindow) * kMel];
-    carry = (float)acc;
-    // SmoothStats: add min(600 - n, 200) / N_g of the global stats
-    float s = carry;
-    if ((double)count < kWindow) {
-      double from_global = kWindow - (double)count;
-      if (from_global > kGlobal) from_global = kGlobal;
-      const float alpha = (float)(from_global / (double)g_count);
-      if (alpha != 1.0f) {
-        s = s + alpha * g;
-        count = count + alpha * g_count;
-      } else {
-        s = s + g;
-        count = count + g_count;
+  for (int t0 = 0; t0 < t_frames; t0 += kTile) {
+    fetch(t0 + kTile, ncur, nold);
+#pragma unroll
+    for (int i = 0; i < kTile; ++i) {
+      const int t = t0 + i;
+      if (t < t_frames) {
+        // ComputeStats (cmvn.cc:35-68): double temp seeded from the float carry
+        double acc = t > 0 ? (double)carry : 0.0;
+        acc += (double)cur[i];
+        if (t >= kWindow) acc += -1.0 * (double)old[i];
+        carry = (float)acc;
+        float s = carry;
+        if (t < kWindow) {
+          const float alpha = s_alpha[t];
+          s = alpha != 1.0f ? s + alpha * g : s + g;
+        }
+        const float neg = s_neg[t < kWindow ? t : kWindow];
+        y[(int64_t)t * kMel] = neg != 1.0f ? cur[i] + neg * s : cur[i] + s;
       }
     }
-    // Apply: scale = 1 / count in double, stored float; feats += -scale * s
-    const float neg = -(float)(1 / (double)count);
-    y[(int64_t)t * kMel] = neg != 1.0f ? xt + neg * s : xt + s;
+#pragma unroll
+    for (int i = 0; i < kTile; ++i) cur[i] = ncur[i], old[i] = nold[i];
   }
 }
 
