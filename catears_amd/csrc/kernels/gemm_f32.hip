@@ -40,7 +40,7 @@ struct KArgs {
   int ldx, ldw, ldy;
   int m, n, k, kpad;
   int din, nseg;
-  int off[8];
+  uint64_t off_packed;  // splice offset of segment s in signed byte s
   int post[4];
   int npost;
   int tiles_m, tiles_n;
@@ -75,19 +75,53 @@ struct Stage {
   f32x4 b[NB];
   float bs[NBS];
 
+  // The splice offsets travel packed in one 64-bit kernel argument (8 signed
+  // bytes) that stays in SGPRs: a dynamically indexed p.off[seg] in the K loop
+  // is an s_load, and a pending scalar load makes hipcc wait lgkmcnt(0) --
+  // behind every outstanding LDS read and write -- before the next use of any
+  // LDS result.
+  __device__ __forceinline__ static int shift_of(const KArgs &p, int seg) {
+    return (int)(signed char)(p.off_packed >> (8 * seg));
+  }
+
+  // Per-thread byte offsets of the staged rows, recomputed only when the
+  // splice segment changes (A) or never (B): a K-tile's loads are then a
+  // wave-uniform base (SGPR) plus a fixed 32-bit VGPR offset, i.e. no vector
+  // address arithmetic between the MFMAs.
+  uint32_t aoff[A_FAST ? NA : 1];
+  uint32_t boff[B_NMAJOR ? 1 : NB];
+  int cur_seg = -1;
+
+  __device__ __forceinline__ void init(const KArgs &p, int n0, int tid) {
+    constexpr int C4 = C::BK / 4;
+    if constexpr (!B_NMAJOR) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const int idx = tid + 256 * i, row = idx / C4, c4 = idx % C4;
+        boff[i] = (uint32_t)((min(n0 + row, p.n - 1) * p.ldw + 4 * c4) * 4);
+      }
+    }
+  }
+
   __device__ __forceinline__ void load(const KArgs &p, int m0, int n0, int k0, int tid) {
     constexpr int C4 = C::BK / 4;
     if constexpr (A_FAST) {
       // whole K-tile inside one splice segment
       const int seg = k0 / p.din, col0 = k0 - seg * p.din;
-      const int shift = p.off[seg];
+      if (seg != cur_seg) {
+        cur_seg = seg;
+        const int shift = shift_of(p, seg);
 #pragma unroll
-      for (int i = 0; i < NA; ++i) {
-        const int idx = tid + 256 * i, row = idx / C4, c4 = idx % C4;
-        int src = clampi(m0 + row + shift, 0, p.m - 1);
-        if constexpr (ROWMAP) src = p.row_map[src];
-        a[i] = *reinterpret_cast<const f32x4 *>(p.x + (int64_t)src * p.ldx + col0 + 4 * c4);
+        for (int i = 0; i < NA; ++i) {
+          const int idx = tid + 256 * i, row = idx / C4, c4 = idx % C4;
+          int src = clampi(m0 + row + shift, 0, p.m - 1);
+          if constexpr (ROWMAP) src = p.row_map[src];
+          aoff[i] = (uint32_t)(src * p.ldx + 4 * c4) * 4u;
+        }
       }
+      const char *base = reinterpret_cast<const char *>(p.x) + (size_t)col0 * 4;
+#pragma unroll
+      for (int i = 0; i < NA; ++i) a[i] = *reinterpret_cast<const f32x4 *>(base + aoff[i]);
     } else {
 #pragma unroll
       for (int i = 0; i < NAS; ++i) {
@@ -96,7 +130,7 @@ struct Stage {
         float v = 0.0f;
         if (kg < p.k) {
           const int seg = kg / p.din, col = kg - seg * p.din;
-          int src = clampi(m0 + row + p.off[seg], 0, p.m - 1);
+          int src = clampi(m0 + row + shift_of(p, seg), 0, p.m - 1);
           if constexpr (ROWMAP) src = p.row_map[src];
           v = p.x[(int64_t)src * p.ldx + col];
         }
@@ -104,12 +138,9 @@ struct Stage {
       }
     }
     if constexpr (!B_NMAJOR) {
+      const char *base = reinterpret_cast<const char *>(p.w) + (size_t)k0 * 4;
 #pragma unroll
-      for (int i = 0; i < NB; ++i) {
-        const int idx = tid + 256 * i, row = idx / C4, c4 = idx % C4;
-        const int nn = min(n0 + row, p.n - 1);
-        b[i] = *reinterpret_cast<const f32x4 *>(p.w + (int64_t)nn * p.ldw + k0 + 4 * c4);
-      }
+      for (int i = 0; i < NB; ++i) b[i] = *reinterpret_cast<const f32x4 *>(base + boff[i]);
     } else {
 #pragma unroll
       for (int i = 0; i < NBS; ++i) {
@@ -183,6 +214,7 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_kernel(KArgs p) {
 
   const int ktiles = p.kpad / BK;
   Stage<C, A_FAST, B_NMAJOR, ROWMAP> st;
+  st.init(p, n0, tid);
   st.load(p, m0, n0, 0, tid);
   st.store(smem, smem + BM * LDT, tid);
   __syncthreads();
@@ -248,6 +280,276 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_kernel(KArgs p) {
   }
 }
 
+// Software-pipelined variant: fragments of k-group g+1 are read from LDS
+// while the MFMAs of group g run, and the single barrier per K-tile sits
+// before the tile's LAST group, so the MFMAs of that group cover the LDS
+// latency of the next tile's first fragments.  The next-next tile's global
+// loads are issued right after the staged registers are written to LDS, a
+// full K-tile ahead of their use.
+//   LDS WAR: buffer b is rewritten in tile kt only after the barrier of tile
+//   kt-1, which every wave passes with lgkmcnt(0) -- i.e. after its last
+//   read of b.  RAW: tile kt+1 is stored before tile kt's barrier and read
+//   after it.
+template <class C, bool A_FAST, bool B_NMAJOR, bool ROWMAP>
+__global__ __launch_bounds__(256, 1) void gemm_f32_pipe_kernel(KArgs p) {
+  __shared__ __attribute__((aligned(16))) float smem[C::SMEM];
+  constexpr int BM = C::BM, BN = C::BN, BK = C::BK, LDT = C::LDT, TI = C::TI, TJ = C::TJ;
+  constexpr int G = BK / 8;
+  static_assert(G >= 2, "pipeline needs >= 2 k-groups per tile");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / C::WGN, wn = wave % C::WGN;
+  int tm, tn;
+  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, &tm, &tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int r = lane & 31, h = lane >> 5;
+  const int a_off = (wm * TI * 32 + r) * LDT + 4 * h;
+  const int b_off = (wn * TJ * 32 + r) * LDT + 4 * h;
+
+  f32x16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+  auto frag = [&](const float *As, int g, f32x4 *fa, f32x4 *fb) {
+    const float *Bs = As + BM * LDT;
+#pragma unroll
+    for (int i = 0; i < TI; ++i) fa[i] = *reinterpret_cast<const f32x4 *>(As + a_off + i * 32 * LDT + g * 8);
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) fb[j] = *reinterpret_cast<const f32x4 *>(Bs + b_off + j * 32 * LDT + g * 8);
+  };
+  auto mma = [&](const f32x4 *fa, const f32x4 *fb) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+  };
+
+  const int ktiles = p.kpad / BK;
+  Stage<C, A_FAST, B_NMAJOR, ROWMAP> st;
+  st.init(p, n0, tid);
+  st.load(p, m0, n0, 0, tid);
+  st.store(smem, smem + BM * LDT, tid);
+  if (ktiles > 1) st.load(p, m0, n0, BK, tid);
+  __syncthreads();
+
+  f32x4 fa0[TI], fb0[TJ], fa1[TI], fb1[TJ];
+  frag(smem, 0, fa0, fb0);
+  for (int kt = 0; kt < ktiles; ++kt) {
+    const float *As = smem + (kt & 1) * (BM + BN) * LDT;
+    float *An = smem + ((kt & 1) ^ 1) * (BM + BN) * LDT;
+    const bool more = kt + 1 < ktiles;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      f32x4 *ca = (g & 1) ? fa1 : fa0, *cb = (g & 1) ? fb1 : fb0;
+      f32x4 *na = (g & 1) ? fa0 : fa1, *nb = (g & 1) ? fb0 : fb1;
+      if (g + 1 < G) {
+        frag(As, g + 1, na, nb);
+      } else if (more) {
+        frag(An, 0, na, nb);  // next tile's first fragments, after the barrier
+      }
+      mma(ca, cb);
+      if (g == G - 2 && more) {
+        st.store(An, An + BM * LDT, tid);
+        __syncthreads();
+        if (kt + 2 < ktiles) st.load(p, m0, n0, (kt + 2) * BK, tid);
+      }
+    }
+    // G is even, so the next tile's group 0 landed in fa0/fb0.
+  }
+
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int col = n0 + wn * TJ * 32 + j * 32 + r;
+    if (col >= p.n) continue;
+    const float bias = p.bias ? p.bias[col] : 0.0f;
+    const float sc = p.bn_scale ? p.bn_scale[col] : 1.0f;
+    const float of = p.bn_offset ? p.bn_offset[col] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = m0 + wm * TI * 32 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (row >= p.m) continue;
+        float v = acc[i][j][e];
+        if (p.bias) v = v + bias;
+        for (int q = 0; q < p.npost; ++q) {
+          if (p.post[q] == kPostRelu) {
+            v = v < 0.0f ? 0.0f : v;
+          } else if (p.post[q] == kPostBatchNorm) {
+            v = v * sc;
+            v = v + of;
+          }
+        }
+        p.y[(int64_t)row * p.ldy + col] = v;
+      }
+    }
+  }
+}
+
+// Pipeline v2 (write-after-barrier, the register-staging schedule of the
+// CDNA guide's T14): staged registers of tile kt+1 are written to LDS right
+// after the MFMAs of tile kt's second k-group are issued (so the ds_writes run
+// under MFMAs), the loads of tile kt+2 are re-issued at once, and the one
+// barrier per tile sits before the last k-group, whose MFMAs cover the LDS
+// latency of tile kt+1's first fragments.
+//   WAR: buffer (kt+1)&1 was last read by tile kt-1's group G-1, whose
+//   fragments every wave fetched (lgkmcnt(0)) before the barrier of kt-1.
+//   RAW: it is written at group 0 of kt and read after the barrier of kt.
+template <class C, bool A_FAST, bool B_NMAJOR, bool ROWMAP>
+__global__ __launch_bounds__(256, 1) void gemm_f32_pipe2_kernel(KArgs p) {
+  __shared__ __attribute__((aligned(16))) float smem[C::SMEM];
+  constexpr int BM = C::BM, BN = C::BN, BK = C::BK, LDT = C::LDT, TI = C::TI, TJ = C::TJ;
+  constexpr int G = BK / 8;
+  static_assert(G >= 4 && G % 2 == 0, "pipeline needs an even number >= 4 of k-groups");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / C::WGN, wn = wave % C::WGN;
+  int tm, tn;
+  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, &tm, &tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int r = lane & 31, h = lane >> 5;
+  const int a_off = (wm * TI * 32 + r) * LDT + 4 * h;
+  const int b_off = (wn * TJ * 32 + r) * LDT + 4 * h;
+
+  f32x16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+  auto frag = [&](const float *As, int g, f32x4 *fa, f32x4 *fb) {
+    const float *Bs = As + BM * LDT;
+#pragma unroll
+    for (int i = 0; i < TI; ++i) fa[i] = *reinterpret_cast<const f32x4 *>(As + a_off + i * 32 * LDT + g * 8);
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) fb[j] = *reinterpret_cast<const f32x4 *>(Bs + b_off + j * 32 * LDT + g * 8);
+  };
+  auto mma = [&](const f32x4 *fa, const f32x4 *fb) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+  };
+
+  const int ktiles = p.kpad / BK;
+  Stage<C, A_FAST, B_NMAJOR, ROWMAP> st;
+  st.init(p, n0, tid);
+  st.load(p, m0, n0, 0, tid);
+  st.store(smem, smem + BM * LDT, tid);
+  if (ktiles > 1) st.load(p, m0, n0, BK, tid);
+  __syncthreads();
+
+  f32x4 fa0[TI], fb0[TJ], fa1[TI], fb1[TJ];
+  frag(smem, 0, fa0, fb0);
+  for (int kt = 0; kt < ktiles; ++kt) {
+    const float *As = smem + (kt & 1) * (BM + BN) * LDT;
+    float *An = smem + ((kt & 1) ^ 1) * (BM + BN) * LDT;
+    const bool more = kt + 1 < ktiles;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      f32x4 *ca = (g & 1) ? fa1 : fa0, *cb = (g & 1) ? fb1 : fb0;
+      f32x4 *na = (g & 1) ? fa0 : fa1, *nb = (g & 1) ? fb0 : fb1;
+      if (g + 1 < G) {
+        frag(As, g + 1, na, nb);
+      } else if (more) {
+        frag(An, 0, na, nb);  // next tile's first fragments, after the barrier
+      }
+      mma(ca, cb);
+      // store after group 1's MFMAs: the wait before group 1 then covers only
+      // its fragment reads, and group 2's wait finds the writes long retired
+      if (g == 1 && more) {
+        st.store(An, An + BM * LDT, tid);
+        if (kt + 2 < ktiles) st.load(p, m0, n0, (kt + 2) * BK, tid);
+      }
+      if (g == G - 2 && more) __syncthreads();
+    }
+  }
+
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int col = n0 + wn * TJ * 32 + j * 32 + r;
+    if (col >= p.n) continue;
+    const float bias = p.bias ? p.bias[col] : 0.0f;
+    const float sc = p.bn_scale ? p.bn_scale[col] : 1.0f;
+    const float of = p.bn_offset ? p.bn_offset[col] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = m0 + wm * TI * 32 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (row >= p.m) continue;
+        float v = acc[i][j][e];
+        if (p.bias) v = v + bias;
+        for (int q = 0; q < p.npost; ++q) {
+          if (p.post[q] == kPostRelu) {
+            v = v < 0.0f ? 0.0f : v;
+          } else if (p.post[q] == kPostBatchNorm) {
+            v = v * sc;
+            v = v + of;
+          }
+        }
+        p.y[(int64_t)row * p.ldy + col] = v;
+      }
+    }
+  }
+}
+
+template <class C>
+int launch_pipe2(hipStream_t s, KArgs p, bool a_fast, bool b_nmajor, bool rm) {
+  p.tiles_n = (p.n + C::BN - 1) / C::BN;
+  p.tiles_m = (p.m + C::BM - 1) / C::BM;
+  if (p.kpad % C::BK != 0) return fail(CE_GPU_EINVAL, "gemm_f32: kpad not a multiple of BK");
+  if (a_fast && p.din % C::BK != 0) a_fast = false;
+  dim3 grid(p.tiles_m * p.tiles_n), block(256);
+  if (a_fast && !b_nmajor && !rm)
+    hipLaunchKernelGGL((gemm_f32_pipe2_kernel<C, true, false, false>), grid, block, 0, s, p);
+  else if (a_fast && !b_nmajor)
+    hipLaunchKernelGGL((gemm_f32_pipe2_kernel<C, true, false, true>), grid, block, 0, s, p);
+  else if (!b_nmajor && rm)
+    hipLaunchKernelGGL((gemm_f32_pipe2_kernel<C, false, false, true>), grid, block, 0, s, p);
+  else if (!b_nmajor)
+    hipLaunchKernelGGL((gemm_f32_pipe2_kernel<C, false, false, false>), grid, block, 0, s, p);
+  else if (a_fast)
+    hipLaunchKernelGGL((gemm_f32_pipe2_kernel<C, true, true, false>), grid, block, 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_f32_pipe2_kernel<C, false, true, false>), grid, block, 0, s, p);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
+template <class C>
+int launch_pipe(hipStream_t s, KArgs p, bool a_fast, bool b_nmajor, bool rm) {
+  p.tiles_n = (p.n + C::BN - 1) / C::BN;
+  p.tiles_m = (p.m + C::BM - 1) / C::BM;
+  if (p.kpad % C::BK != 0) return fail(CE_GPU_EINVAL, "gemm_f32: kpad not a multiple of BK");
+  if (a_fast && p.din % C::BK != 0) a_fast = false;
+  dim3 grid(p.tiles_m * p.tiles_n), block(256);
+  if (a_fast && !b_nmajor && !rm)
+    hipLaunchKernelGGL((gemm_f32_pipe_kernel<C, true, false, false>), grid, block, 0, s, p);
+  else if (a_fast && !b_nmajor)
+    hipLaunchKernelGGL((gemm_f32_pipe_kernel<C, true, false, true>), grid, block, 0, s, p);
+  else if (!b_nmajor && rm)
+    hipLaunchKernelGGL((gemm_f32_pipe_kernel<C, false, false, true>), grid, block, 0, s, p);
+  else if (!b_nmajor)
+    hipLaunchKernelGGL((gemm_f32_pipe_kernel<C, false, false, false>), grid, block, 0, s, p);
+  else if (a_fast)
+    hipLaunchKernelGGL((gemm_f32_pipe_kernel<C, true, true, false>), grid, block, 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_f32_pipe_kernel<C, false, true, false>), grid, block, 0, s, p);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
 template <class C>
 int launch_cfg(hipStream_t s, KArgs p, bool a_fast, bool b_nmajor, bool rm) {
   p.tiles_n = (p.n + C::BN - 1) / C::BN;
@@ -277,6 +579,7 @@ using V1 = Cfg<128, 128, 64, 2, 2>;
 using V2 = Cfg<128, 64, 32, 2, 2>;
 using V3 = Cfg<64, 128, 32, 2, 2>;
 using V4 = Cfg<128, 64, 64, 2, 2>;
+using V8 = Cfg<64, 64, 32, 2, 2>;
 
 int variant() {
   static int v = [] {
@@ -313,7 +616,11 @@ int launch_gemm_f32(hipStream_t s, const GemmArgs &a) {
   p.kpad = a.kpad;
   p.din = a.din;
   p.nseg = a.nseg;
-  for (int i = 0; i < 8; ++i) p.off[i] = a.off[i];
+  p.off_packed = 0;
+  for (int i = 0; i < a.nseg; ++i) {
+    if (a.off[i] < -128 || a.off[i] > 127) return fail(CE_GPU_ENOTSUP, "gemm_f32: splice offset beyond +-127");
+    p.off_packed |= (uint64_t)(uint8_t)(int8_t)a.off[i] << (8 * i);
+  }
   for (int i = 0; i < 4; ++i) p.post[i] = a.post[i];
   p.npost = a.npost;
   // fast A path: every K-tile inside one segment, float4-aligned rows
@@ -322,6 +629,11 @@ int launch_gemm_f32(hipStream_t s, const GemmArgs &a) {
     return fail(CE_GPU_EINVAL, "gemm_f32: K-major B must be 16-byte aligned");
   const bool rm = a.row_map != nullptr;
   if (a.b_nmajor && rm) return fail(CE_GPU_EINVAL, "gemm_f32: row_map needs K-major weights");
+  // staged loads use 32-bit byte offsets from a uniform base
+  if (!a.b_nmajor && (int64_t)a.n * a.ldw * 4 >= (int64_t)1 << 32)
+    return fail(CE_GPU_EINVAL, "gemm_f32: weight matrix beyond 4 GiB");
+  if (a_fast && (int64_t)(a.row_map ? INT32_MAX / 4 : a.m) * a.ldx * 4 >= (int64_t)1 << 32 && !a.row_map)
+    return fail(CE_GPU_EINVAL, "gemm_f32: activation block beyond 4 GiB");
   // K-tiles deeper than 32 only where K allows it
   const bool deep = a.kpad % 64 == 0;
   switch (variant()) {
@@ -333,6 +645,30 @@ int launch_gemm_f32(hipStream_t s, const GemmArgs &a) {
       return launch_cfg<V3>(s, p, a_fast, a.b_nmajor, rm);
     case 4:
       return deep ? launch_cfg<V4>(s, p, a_fast, a.b_nmajor, rm) : launch_cfg<V2>(s, p, a_fast, a.b_nmajor, rm);
+    case 5:
+      return launch_pipe<V0>(s, p, a_fast, a.b_nmajor, rm);
+    case 6:
+      return launch_pipe<V2>(s, p, a_fast, a.b_nmajor, rm);
+    case 7:
+      return launch_pipe<V3>(s, p, a_fast, a.b_nmajor, rm);
+    case 8:
+      return launch_cfg<V8>(s, p, a_fast, a.b_nmajor, rm);
+    case 9:
+      return launch_pipe<V8>(s, p, a_fast, a.b_nmajor, rm);
+    case 10:
+      return deep ? launch_pipe<V1>(s, p, a_fast, a.b_nmajor, rm) : launch_pipe<V0>(s, p, a_fast, a.b_nmajor, rm);
+    case 11:
+      return launch_pipe2<V0>(s, p, a_fast, a.b_nmajor, rm);
+    case 12:
+      return launch_pipe2<V2>(s, p, a_fast, a.b_nmajor, rm);
+    case 13:
+      return launch_pipe2<V3>(s, p, a_fast, a.b_nmajor, rm);
+    case 14:
+      return launch_pipe2<V8>(s, p, a_fast, a.b_nmajor, rm);
+    case 15:
+      return deep ? launch_pipe2<V1>(s, p, a_fast, a.b_nmajor, rm) : launch_pipe2<V0>(s, p, a_fast, a.b_nmajor, rm);
+    case 16:
+      return deep ? launch_pipe2<V4>(s, p, a_fast, a.b_nmajor, rm) : launch_pipe2<V2>(s, p, a_fast, a.b_nmajor, rm);
     default:
       return launch_cfg<V0>(s, p, a_fast, a.b_nmajor, rm);
   }
