@@ -54,12 +54,16 @@ __global__ __launch_bounds__(64) void cmvn_kernel(const int64_t *__restrict__ fr
   const float *x = in + r0 * kMel + d;
   float *y = out + r0 * kMel + d;
   float cur[kTile], old[kTile], ncur[kTile], nold[kTile];
+  // Unconditional loads at clamped (always valid) frames: a per-element
+  // "load or zero" select makes hipcc branch around every load and wait
+  // vmcnt(0) each time.  Frames past the end are never used.
+  if (t_frames == 0) return;
   auto fetch = [&](int t0, float *c, float *o) {
 #pragma unroll
     for (int i = 0; i < kTile; ++i) {
-      const int t = t0 + i;
-      c[i] = t < t_frames ? x[(int64_t)t * kMel] : 0.0f;
-      o[i] = (t >= kWindow && t < t_frames) ? x[(int64_t)(t - kWindow) * kMel] : 0.0f;
+      const int t = min(t0 + i, t_frames - 1);
+      c[i] = x[(int64_t)t * kMel];
+      o[i] = x[(int64_t)max(t - kWindow, 0) * kMel];
     }
   };
   fetch(0, cur, old);

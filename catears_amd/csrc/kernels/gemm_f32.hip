@@ -581,10 +581,14 @@ using V3 = Cfg<64, 128, 32, 2, 2>;
 using V4 = Cfg<128, 64, 64, 2, 2>;
 using V8 = Cfg<64, 64, 32, 2, 2>;
 
+// Default: write-after-barrier pipeline on 64 x 128 tiles (measured best on
+// TDNN-S, tools/gemm_variants.sh); CATEARS_GEMM_VARIANT overrides for tuning.
+constexpr int kDefaultVariant = 13;
+
 int variant() {
   static int v = [] {
     const char *e = getenv("CATEARS_GEMM_VARIANT");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : kDefaultVariant;
   }();
   return v;
 }
