@@ -66,10 +66,22 @@ __global__ __launch_bounds__(64) void cmvn_kernel(const int64_t *__restrict__ fr
       o[i] = x[(int64_t)max(t - kWindow, 0) * kMel];
     }
   };
+  // per-frame scalars of a tile, read from LDS before the chain runs (a read
+  // per step would put an LDS round trip on the critical path)
+  float al[kTile], ng[kTile];
+  auto scalars = [&](int t0) {
+#pragma unroll
+    for (int i = 0; i < kTile; ++i) {
+      const int t = t0 + i;
+      al[i] = s_alpha[min(t, kWindow - 1)];
+      ng[i] = s_neg[min(t, kWindow)];
+    }
+  };
   fetch(0, cur, old);
   float carry = 0.0f;
   for (int t0 = 0; t0 < t_frames; t0 += kTile) {
     fetch(t0 + kTile, ncur, nold);
+    scalars(t0);
 #pragma unroll
     for (int i = 0; i < kTile; ++i) {
       const int t = t0 + i;
@@ -80,12 +92,8 @@ __global__ __launch_bounds__(64) void cmvn_kernel(const int64_t *__restrict__ fr
         if (t >= kWindow) acc += -1.0 * (double)old[i];
         carry = (float)acc;
         float s = carry;
-        if (t < kWindow) {
-          const float alpha = s_alpha[t];
-          s = alpha != 1.0f ? s + alpha * g : s + g;
-        }
-        const float neg = s_neg[t < kWindow ? t : kWindow];
-        y[(int64_t)t * kMel] = neg != 1.0f ? cur[i] + neg * s : cur[i] + s;
+        if (t < kWindow) s = al[i] != 1.0f ? s + al[i] * g : s + g;
+        y[(int64_t)t * kMel] = ng[i] != 1.0f ? cur[i] + ng[i] * s : cur[i] + s;
       }
     }
 #pragma unroll
