@@ -94,6 +94,7 @@ def main():
     import torch.distributed as dist
 
     from catears_amd import gpu, synth
+    from catears_amd.shard import LoglikGather
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -138,10 +139,7 @@ def main():
     outs = [torch.empty((frames_per_step, model.num_pdfs), dtype=torch.float32, device="cuda")
             for _ in range(nbuf)]
     gather = world > 1 and not args.no_gather
-    recv = None
-    if gather and rank == 0:
-        recv = [[torch.empty_like(outs[0]) for _ in range(world)] for _ in range(nbuf)]
-    pending = [None] * nbuf
+    gat = LoglikGather(outs[0].shape, torch.float32, "cuda", depth=nbuf) if gather else None
     checksum = torch.zeros((), dtype=torch.float64, device="cuda")
 
     def front_stage(i):
@@ -156,14 +154,13 @@ def main():
 
     def back_stage(i):
         slot, o = i % 2, i % nbuf
-        if pending[o] is not None:
-            pending[o].wait()  # gather from nbuf steps ago has read this buffer
-            pending[o] = None
+        if gat is not None:
+            gat.wait_slot(o)  # the gather from nbuf steps ago has read outs[o]
         back.wait_event(ready[slot])
         gpu.am_forward(ctx, model, plan, norm[slot], outs[o])
         free[slot].record(back)
-        if gather:
-            pending[o] = dist.gather(outs[o], recv[o] if rank == 0 else None, dst=0, async_op=True)
+        if gat is not None:
+            assert gat.submit(outs[o]) == o
 
     def run(first, count):
         front_stage(first)
@@ -173,10 +170,8 @@ def main():
             back_stage(i)
 
     run(0, args.warmup)
-    for w in pending:
-        if w is not None:
-            w.wait()
-    pending = [None] * nbuf
+    if gat is not None:
+        gat.drain()
     torch.cuda.synchronize()
     if not args.no_profile:
         ctx.profile(True)
@@ -186,9 +181,8 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run(args.warmup, args.steps)
-    for w in pending:
-        if w is not None:
-            w.wait()
+    if gat is not None:
+        gat.drain()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -197,6 +191,8 @@ def main():
         elapsed = float(t.item())
     # the outputs are consumed (checksum) so no work can be elided
     checksum += outs[(args.warmup + args.steps - 1) % nbuf].double().sum()
+    if gat is not None:
+        checksum += gat.checksum
     finite = bool(torch.isfinite(outs[0]).all().item())
 
     prof = {}
@@ -226,7 +222,7 @@ def main():
             achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
             roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": MFMA_F32_PEAK_TFLOPS,
                         "unit": "TFLOP/s", "frac": round(achieved / MFMA_F32_PEAK_TFLOPS, 4),
-                        "traffic": None, "kernel": "gemm_f32_kernel<true,false> (TDNN layers 2-7)",
+                        "traffic": None, "kernel": "gemm_f32_pipe2_kernel<Cfg<64,128,32,2,2>,true,false,false> (TDNN layers 2-7)",
                         "launches": n, "avg_launch_ms": round(avg_ms, 4),
                         "flops_per_launch": flops_per_launch}
         for name, (ms, n) in prof.items():
