@@ -45,3 +45,32 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean
+
+# ---------------------------------------------------------------------------
+# Drop-in pocketkaldi classes (C++ host layer over the C-ABI).  compat/ holds
+# stand-ins for the reference's container headers, used only when building
+# outside the reference tree (a reference build finds its own first).
+HOST := catears_amd/host
+PKLIB := catears_amd/lib/libcatears_pk.so
+PKINC := -I$(HOST)/include -I$(HOST)/compat -Iinclude -I/opt/rocm/include
+PKFLAGS := -O2 -fPIC -std=c++17 -ffp-contract=off -D__HIP_PLATFORM_AMD__ -Wall $(PKINC)
+PKSRC := $(wildcard $(HOST)/src/*.cc) $(wildcard $(HOST)/compat_src/*.cc)
+PKOBJS := $(patsubst $(HOST)/%.cc,$(OBJ)/host/%.o,$(PKSRC))
+PKHDRS := $(wildcard $(HOST)/include/*.h) $(wildcard $(HOST)/compat/*.h) include/catears_gpu.h
+PKTEST := catears_amd/lib/pk_dropin
+
+$(OBJ)/host/%.o: $(HOST)/%.cc $(PKHDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(PKFLAGS) -c $< -o $@
+
+$(PKLIB): $(PKOBJS) $(LIB)
+	$(CXX) -shared -o $@ $(PKOBJS) -Lcatears_amd/lib -lcatears_hip -L/opt/rocm/lib -lamdhip64 \
+	    -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,/opt/rocm/lib -Wl,--no-undefined
+
+$(PKTEST): tests/native/pk_dropin.cc $(PKLIB) $(PKHDRS)
+	$(CXX) $(PKFLAGS) -o $@ $< -Lcatears_amd/lib -lcatears_pk -lcatears_hip -L/opt/rocm/lib -lamdhip64 \
+	    -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,/opt/rocm/lib
+
+host: $(PKLIB) $(PKTEST)
+all: host
+.PHONY: host

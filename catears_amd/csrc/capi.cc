@@ -84,6 +84,13 @@ struct Reader {
     if (!f) return fail(CE_GPU_EIO, "IOError: Unable to open " + path);
     return CE_GPU_OK;
   }
+  // The same over an in-memory image (ce_gpu_model_load_mem).
+  int open_mem(const void *buf, size_t n, const char *label) {
+    name = label;
+    f = n ? fmemopen(const_cast<void *>(buf), n, "rb") : nullptr;
+    if (!f) return fail(CE_GPU_EIO, std::string("IOError: Unable to open ") + label);
+    return CE_GPU_OK;
+  }
   int read(void *dst, size_t n) {
     if (n == 0) return CE_GPU_OK;
     if (fread(dst, n, 1, f) != 1) return fail(CE_GPU_EIO, "IOError: failed to read: " + name);
@@ -206,9 +213,8 @@ struct RawLayer {
 };
 
 // Nnet::Read / ReadLayer (src/nnet.cc:221-293)
-static int read_nnet(const std::string &path, std::vector<RawLayer> *layers, int *hl, int *hr) {
-  Reader rd;
-  CE_TRY(rd.open(path));
+static int read_nnet(Reader &rd, std::vector<RawLayer> *layers, int *hl, int *hr) {
+  const std::string &path = rd.name;
   CE_TRY(rd.tag("NN02"));
   int32_t l = 0, r = 0, n = 0;
   CE_TRY(rd.i32(&l));
@@ -370,35 +376,55 @@ static int build_program(const std::vector<RawLayer> &layers, int left, int righ
   }
   if (m->steps.empty() || !m->steps.front().is_gemm)
     return fail(CE_GPU_ENOTSUP, "the nnet must start with a (spliced) Linear layer");
-  if (sum_l != left || sum_r != right)
+  m->net_left = sum_l;
+  m->net_right = sum_r;
+  if (left < 0 && right < 0) {
+    m->left = sum_l;
+    m->right = sum_r;
+  } else if (sum_l != left || sum_r != right)
     return fail(CE_GPU_ECORRUPT, fmt("Corruption: config context (%d, %d) differs from the nnet's (%d, %d)",
                                      left, right, sum_l, sum_r));
   m->num_pdfs = width;
   return CE_GPU_OK;
 }
 
-static int load_model(ce_gpu_ctx *ctx, const std::string &nnet, const std::string &prior, int left,
-                      int right, const std::string &tid2pdf, ce_gpu_model **out) {
+// Nnet::Read into a device program; `rd` is positioned at the NN02 tag.
+// left/right < 0: take the context from the network's Narrow layers.
+static int read_program(ce_gpu_ctx *ctx, Reader &rd, int left, int right, ce_gpu_model *m) {
   CE_HIP(hipSetDevice(ctx->device));
-  std::unique_ptr<ce_gpu_model> m(new (std::nothrow) ce_gpu_model());
-  if (!m) return fail(CE_GPU_ENOMEM, "out of host memory");
-  if (left < 0 || right < 0) return fail(CE_GPU_EINVAL, "negative context");
+  if ((left < 0) != (right < 0)) return fail(CE_GPU_EINVAL, "negative context");
   m->left = left;
   m->right = right;
   std::vector<RawLayer> layers;
   int hl = 0, hr = 0;
-  CE_TRY(read_nnet(nnet, &layers, &hl, &hr));
-  CE_TRY(build_program(layers, left, right, m.get()));
-  // prior: VEC0, then ApplyLog (src/am.cc:40-44)
-  Reader rd;
-  CE_TRY(rd.open(prior));
+  CE_TRY(read_nnet(rd, &layers, &hl, &hr));
+  return build_program(layers, left, right, m);
+}
+
+// Prior probabilities -> device log prior (ApplyLog, src/am.cc:40-44).
+static int set_prior(ce_gpu_model *m, const float *prior, int dim) {
+  if (dim != m->num_pdfs)
+    return fail(CE_GPU_ECORRUPT, fmt("Corruption: prior has %d entries, nnet outputs %d", dim, m->num_pdfs));
+  std::vector<float> lp(prior, prior + dim);
+  for (float &v : lp) v = logf(v);
+  return m->log_prior.upload(lp.data(), lp.size() * 4);
+}
+
+static int load_model(ce_gpu_ctx *ctx, const std::string &nnet, const std::string &prior, int left,
+                      int right, const std::string &tid2pdf, ce_gpu_model **out) {
+  std::unique_ptr<ce_gpu_model> m(new (std::nothrow) ce_gpu_model());
+  if (!m) return fail(CE_GPU_ENOMEM, "out of host memory");
+  if (left < 0 || right < 0) return fail(CE_GPU_EINVAL, "negative context");
+  {
+    Reader rd;
+    CE_TRY(rd.open(nnet));
+    CE_TRY(read_program(ctx, rd, left, right, m.get()));
+  }
+  Reader rp;
+  CE_TRY(rp.open(prior));
   std::vector<float> pr;
-  CE_TRY(rd.vec(&pr));
-  if ((int)pr.size() != m->num_pdfs)
-    return fail(CE_GPU_ECORRUPT, fmt("Corruption: prior has %d entries, nnet outputs %d", (int)pr.size(),
-                                     m->num_pdfs));
-  for (float &v : pr) v = logf(v);
-  CE_TRY(m->log_prior.upload(pr.data(), pr.size() * 4));
+  CE_TRY(rp.vec(&pr));
+  CE_TRY(set_prior(m.get(), pr.data(), (int)pr.size()));
   if (!tid2pdf.empty()) {
     Reader rt;
     CE_TRY(rt.open(tid2pdf));
@@ -712,6 +738,62 @@ int ce_gpu_cmvn(ce_gpu_ctx *ctx, const ce_gpu_plan *p, const float *d_global_sta
   return launch_cmvn(ctx->stream, p, d_global_stats, d_feats, d_out);
 }
 
+}  // extern "C"
+
+namespace catears {
+// Runs the program's steps on `rows` packed rows starting at x (row_map: the
+// first layer's packed row -> source row, or NULL for identity).  Returns the
+// last activation via *y / *ldy.
+static int run_steps(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, int ldx, int rows,
+                     const int *row_map, const float **y, int *ldy) {
+  const size_t per = (size_t)rows * m->max_width;
+  CE_TRY(ensure_workspace(ctx, 2 * per));
+  float *buf[2] = {ctx->workspace.as<float>(), ctx->workspace.as<float>() + per};
+  int cur = 0;
+  bool first = true;
+  for (const Step &st : m->steps) {
+    if (st.is_gemm) {
+      const GemmLayer &g = st.gemm;
+      GemmArgs a;
+      a.x = x;
+      a.ldx = ldx;
+      a.row_map = first ? row_map : nullptr;
+      a.m = rows;
+      a.n = g.n;
+      a.k = g.k;
+      a.kpad = g.kpad;
+      a.din = g.din;
+      a.nseg = g.nseg;
+      for (int i = 0; i < 8; ++i) a.off[i] = g.off[i];
+      a.w = g.wt.as<float>();
+      a.ldw = g.kpad;
+      a.bias = g.bias.as<float>();
+      a.bn_scale = g.bn_scale.as<float>();
+      a.bn_offset = g.bn_offset.as<float>();
+      for (int i = 0; i < 4; ++i) a.post[i] = g.post[i];
+      a.npost = g.npost;
+      a.y = buf[cur];
+      a.ldy = g.n;
+      {
+        ProfScope prof(ctx, g.din % 32 == 0 ? CE_GPU_PROF_GEMM : CE_GPU_PROF_GEMM_GATHER);
+        CE_TRY(launch_gemm_f32(ctx->stream, a));
+      }
+      x = buf[cur];
+      ldx = g.n;
+      cur ^= 1;
+      first = false;
+    } else {
+      CE_TRY(launch_rowop(ctx->stream, st.row, const_cast<float *>(x), ldx, rows));
+    }
+  }
+  *y = x;
+  *ldy = ldx;
+  return CE_GPU_OK;
+}
+}  // namespace catears
+
+extern "C" {
+
 int ce_gpu_am_forward(ce_gpu_ctx *ctx, const ce_gpu_model *m, const ce_gpu_plan *p, const float *d_feats,
                       float *d_loglik) {
   if (!ctx || !m || !p) return fail(CE_GPU_EINVAL, "NULL argument");
@@ -719,55 +801,53 @@ int ce_gpu_am_forward(ce_gpu_ctx *ctx, const ce_gpu_model *m, const ce_gpu_plan 
     return fail(CE_GPU_EINVAL, "plan was not built for this model's context");
   if (p->chunks.empty()) return CE_GPU_OK;
   if (!d_feats || !d_loglik) return fail(CE_GPU_EINVAL, "NULL argument");
-  const size_t per = (size_t)p->max_chunk_rows * m->max_width;
-  CE_TRY(ensure_workspace(ctx, 2 * per));
-  float *buf[2] = {ctx->workspace.as<float>(), ctx->workspace.as<float>() + per};
+  if (!m->log_prior.ptr) return fail(CE_GPU_EINVAL, "am_forward needs a model loaded with a prior");
+  if (m->left != m->net_left || m->right != m->net_right)
+    return fail(CE_GPU_EINVAL, "model context differs from its network's");
   for (const ce_gpu_plan::Chunk &c : p->chunks) {
     const int *row_src = p->d_row_src.as<int>() + c.map_base;
     const int *row_dst = p->d_row_dst.as<int>() + c.map_base;
-    const float *x = d_feats;
-    int ldx = m->input_dim, cur = 0;
-    bool first = true;
-    for (const Step &st : m->steps) {
-      if (st.is_gemm) {
-        const GemmLayer &g = st.gemm;
-        GemmArgs a;
-        a.x = x;
-        a.ldx = ldx;
-        a.row_map = first ? row_src : nullptr;
-        a.m = c.rows;
-        a.n = g.n;
-        a.k = g.k;
-        a.kpad = g.kpad;
-        a.din = g.din;
-        a.nseg = g.nseg;
-        for (int i = 0; i < 8; ++i) a.off[i] = g.off[i];
-        a.w = g.wt.as<float>();
-        a.ldw = g.kpad;
-        a.bias = g.bias.as<float>();
-        a.bn_scale = g.bn_scale.as<float>();
-        a.bn_offset = g.bn_offset.as<float>();
-        for (int i = 0; i < 4; ++i) a.post[i] = g.post[i];
-        a.npost = g.npost;
-        a.y = buf[cur];
-        a.ldy = g.n;
-        {
-          ProfScope prof(ctx, g.din % 32 == 0 ? CE_GPU_PROF_GEMM : CE_GPU_PROF_GEMM_GATHER);
-          CE_TRY(launch_gemm_f32(ctx->stream, a));
-        }
-        x = buf[cur];
-        ldx = g.n;
-        cur ^= 1;
-        first = false;
-      } else {
-        CE_TRY(launch_rowop(ctx->stream, st.row, const_cast<float *>(x), ldx, c.rows));
-      }
-    }
+    const float *y = nullptr;
+    int ldy = 0;
+    CE_TRY(run_steps(ctx, m, d_feats, m->input_dim, c.rows, row_src, &y, &ldy));
     ProfScope prof(ctx, CE_GPU_PROF_FINALIZE);
-    CE_TRY(launch_finalize(ctx->stream, x, ldx, c.rows, m->num_pdfs, m->final_log_softmax,
+    CE_TRY(launch_finalize(ctx->stream, y, ldy, c.rows, m->num_pdfs, m->final_log_softmax,
                            m->log_prior.as<float>(), row_dst, d_loglik));
   }
   return CE_GPU_OK;
+}
+
+int ce_gpu_model_load_mem(ce_gpu_ctx *ctx, const void *nnet, int64_t nbytes, const float *h_prior,
+                          int prior_dim, int left_context, int right_context, ce_gpu_model **out) {
+  if (!ctx || !out || !nnet || nbytes <= 0 || (prior_dim > 0 && !h_prior))
+    return fail(CE_GPU_EINVAL, "bad argument");
+  *out = nullptr;
+  std::unique_ptr<ce_gpu_model> m(new (std::nothrow) ce_gpu_model());
+  if (!m) return fail(CE_GPU_ENOMEM, "out of host memory");
+  Reader rd;
+  CE_TRY(rd.open_mem(nnet, (size_t)nbytes, "<nnet image>"));
+  CE_TRY(read_program(ctx, rd, left_context, right_context, m.get()));
+  if (h_prior) CE_TRY(set_prior(m.get(), h_prior, prior_dim));
+  *out = m.release();
+  return CE_GPU_OK;
+}
+
+int ce_gpu_nnet_propagate(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *d_in, int rows, int ld_in,
+                          int subtract_prior, float *d_out) {
+  if (!ctx || !m || !d_in || !d_out) return fail(CE_GPU_EINVAL, "NULL argument");
+  if (ld_in < m->input_dim) return fail(CE_GPU_EINVAL, "ld_in smaller than the nnet input");
+  const int out_rows = rows - m->net_left - m->net_right;
+  if (out_rows <= 0)
+    return fail(CE_GPU_EINVAL, fmt("nnet_propagate: %d rows do not cover the network context (%d, %d)", rows,
+                                   m->net_left, m->net_right));
+  if (subtract_prior && !m->log_prior.ptr) return fail(CE_GPU_EINVAL, "model has no prior");
+  const float *y = nullptr;
+  int ldy = 0;
+  CE_TRY(run_steps(ctx, m, d_in, ld_in, rows, nullptr, &y, &ldy));
+  ProfScope prof(ctx, CE_GPU_PROF_FINALIZE);
+  return launch_finalize(ctx->stream, y + (size_t)m->net_left * ldy, ldy, out_rows, m->num_pdfs,
+                         m->final_log_softmax, subtract_prior ? m->log_prior.as<float>() : nullptr, nullptr,
+                         d_out);
 }
 
 int ce_gpu_score(ce_gpu_ctx *ctx, const ce_gpu_model *m, const ce_gpu_plan *p, const float *d_pcm,
@@ -832,6 +912,56 @@ int ce_gpu_gemm_u8u8f32(ce_gpu_ctx *ctx, int m, int n, int k, const uint8_t *d_a
 int ce_gpu_gemm_u8u8i32(ce_gpu_ctx *ctx, int m, int n, int k, const uint8_t *d_a, const void *d_params_a,
                         const uint8_t *d_b, const void *d_params_b, int32_t *d_c) {
   return gemm_u8(ctx, m, n, k, d_a, d_params_a, d_b, d_params_b, nullptr, d_c);
+}
+
+static_assert(kRowRelu == CE_GPU_ROW_RELU && kRowBatchNorm == CE_GPU_ROW_BATCHNORM &&
+                  kRowLogSoftmax == CE_GPU_ROW_LOGSOFTMAX && kRowSoftmax == CE_GPU_ROW_SOFTMAX &&
+                  kRowNormalize == CE_GPU_ROW_NORMALIZE,
+              "row-op numbering");
+
+int ce_gpu_linear(ce_gpu_ctx *ctx, int rows, int in_dim, int out_dim, const float *d_in, int ld_in,
+                  const float *d_w, int ld_w, const float *d_b, float *d_out, int ld_out) {
+  if (!ctx || rows < 0 || in_dim < 0 || out_dim < 0) return fail(CE_GPU_EINVAL, "bad argument");
+  if (rows == 0 || out_dim == 0) return CE_GPU_OK;
+  if (!d_in || !d_w || !d_out) return fail(CE_GPU_EINVAL, "NULL argument");
+  if (in_dim == 0) return fail(CE_GPU_EINVAL, "linear: empty input");
+  if (ld_in < in_dim || ld_w < out_dim || ld_out < out_dim) return fail(CE_GPU_EINVAL, "leading dimension too small");
+  GemmArgs a;
+  a.x = d_in;
+  a.ldx = ld_in;
+  a.m = rows;
+  a.n = out_dim;
+  a.k = in_dim;
+  a.kpad = (in_dim + gemm_k_align() - 1) / gemm_k_align() * gemm_k_align();
+  a.din = in_dim;
+  a.nseg = 1;
+  a.w = d_w;
+  a.ldw = ld_w;
+  a.b_nmajor = true;
+  a.bias = d_b;
+  a.y = d_out;
+  a.ldy = ld_out;
+  ProfScope prof(ctx, CE_GPU_PROF_GEMM_GATHER);
+  return launch_gemm_f32(ctx->stream, a);
+}
+
+int ce_gpu_splice(ce_gpu_ctx *ctx, int rows, int dim, const float *d_in, int ld_in, const int32_t *h_idx,
+                  int n_idx, float *d_out) {
+  if (!ctx || rows < 0 || dim < 0 || n_idx < 1 || n_idx > CE_GPU_MAX_SPLICE || !h_idx)
+    return fail(CE_GPU_EINVAL, "bad argument");
+  if (rows == 0 || dim == 0) return CE_GPU_OK;
+  if (!d_in || !d_out || ld_in < dim) return fail(CE_GPU_EINVAL, "bad operand");
+  return launch_splice(ctx->stream, rows, dim, d_in, ld_in, h_idx, n_idx, d_out);
+}
+
+int ce_gpu_rowwise(ce_gpu_ctx *ctx, int op, int rows, int dim, float *d_x, int ld, const float *d_scale,
+                   const float *d_offset) {
+  if (!ctx || rows < 0 || dim < 0 || ld < dim) return fail(CE_GPU_EINVAL, "bad argument");
+  if (op < CE_GPU_ROW_RELU || op > CE_GPU_ROW_NORMALIZE) return fail(CE_GPU_EINVAL, "unknown row op");
+  if (op == CE_GPU_ROW_BATCHNORM && (!d_scale || !d_offset)) return fail(CE_GPU_EINVAL, "BatchNorm needs scale/offset");
+  if (rows == 0 || dim == 0) return CE_GPU_OK;
+  if (!d_x) return fail(CE_GPU_EINVAL, "NULL argument");
+  return launch_rowop_raw(ctx->stream, op, dim, d_scale, d_offset, d_x, ld, rows);
 }
 
 }  // extern "C"

@@ -107,6 +107,7 @@ struct GemmLayer {
   int npost = 0;
 };
 
+// Same numbering as the ABI's CE_GPU_ROW_* (checked in capi.cc).
 enum RowOpKind : int { kRowRelu, kRowBatchNorm, kRowLogSoftmax, kRowSoftmax, kRowNormalize };
 
 struct RowOp {
@@ -156,7 +157,8 @@ struct ProfScope {
 }  // namespace catears
 
 struct ce_gpu_model {
-  int left = 0, right = 0, chunk = 0;
+  int left = 0, right = 0, chunk = 0;  // context the caller pads with (config)
+  int net_left = 0, net_right = 0;     // rows the Narrow layers drop
   int input_dim = 0, num_pdfs = 0, num_linear = 0, max_width = 0;
   int64_t num_params = 0;
   bool final_log_softmax = false;
@@ -218,6 +220,10 @@ int gemm_k_align();
 int launch_finalize(hipStream_t s, const float *x, int ldx, int rows, int dim, bool log_softmax,
                     const float *log_prior, const int *row_dst, float *out);
 int launch_rowop(hipStream_t s, const RowOp &op, float *x, int ldx, int rows);
+int launch_rowop_raw(hipStream_t s, int kind, int dim, const float *scale, const float *offset, float *x,
+                     int ldx, int rows);
+int launch_splice(hipStream_t s, int rows, int dim, const float *in, int ld_in, const int32_t *h_idx,
+                  int n_idx, float *out);
 
 int launch_quantize(hipStream_t s, const float *x, int64_t count, uint8_t *q, void *params,
                     void *scratch);

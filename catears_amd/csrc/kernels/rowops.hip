@@ -50,7 +50,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(const float *__restrict__
       if (c < dim) {
         float y = v[j];
         if (LOGSM) y = y - ls;
-        o[c] = y - prior[c];
+        o[c] = prior ? y - prior[c] : y;
       }
     }
   } else {
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(const float *__restrict__
     for (int c = lane; c < dim; c += 64) {
       float y = xr[c];
       if (LOGSM) y = y - ls;
-      o[c] = y - prior[c];
+      o[c] = prior ? y - prior[c] : y;
     }
   }
 }
@@ -109,7 +109,35 @@ __global__ __launch_bounds__(256) void rowop_kernel(int kind, float *__restrict_
   }
 }
 
+// SpliceLayer::Propagate (src/nnet.cc:50-95): out[t] = concat over s of
+// in[clamp(t + idx[s], 0, rows - 1)].  One block per output row; a pure copy.
+struct SpliceIdx {
+  int v[CE_GPU_MAX_SPLICE];
+};
+
+__global__ __launch_bounds__(256) void splice_kernel(int rows, int dim, const float *__restrict__ in, int ld_in,
+                                                     SpliceIdx idx, int n_idx, float *__restrict__ out) {
+  const int t = blockIdx.x;
+  const int width = dim * n_idx;
+  float *o = out + (int64_t)t * width;
+  for (int c = threadIdx.x; c < width; c += blockDim.x) {
+    const int s = c / dim, j = c - s * dim;
+    int src = t + idx.v[s];
+    src = src < 0 ? 0 : (src > rows - 1 ? rows - 1 : src);
+    o[c] = in[(int64_t)src * ld_in + j];
+  }
+}
+
 }  // namespace
+
+int launch_splice(hipStream_t s, int rows, int dim, const float *in, int ld_in, const int32_t *h_idx,
+                  int n_idx, float *out) {
+  SpliceIdx idx = {};
+  for (int i = 0; i < n_idx; ++i) idx.v[i] = h_idx[i];
+  hipLaunchKernelGGL(splice_kernel, dim3(rows), dim3(256), 0, s, rows, dim, in, ld_in, idx, n_idx, out);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
 
 int launch_finalize(hipStream_t s, const float *x, int ldx, int rows, int dim, bool log_softmax,
                     const float *log_prior, const int *row_dst, float *out) {
@@ -125,12 +153,17 @@ int launch_finalize(hipStream_t s, const float *x, int ldx, int rows, int dim, b
   return CE_GPU_OK;
 }
 
-int launch_rowop(hipStream_t s, const RowOp &op, float *x, int ldx, int rows) {
+int launch_rowop_raw(hipStream_t s, int kind, int dim, const float *scale, const float *offset, float *x,
+                     int ldx, int rows) {
   if (rows <= 0) return CE_GPU_OK;
-  hipLaunchKernelGGL(rowop_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, op.kind, x, ldx, rows,
-                     op.dim, op.scale.as<float>(), op.offset.as<float>());
+  hipLaunchKernelGGL(rowop_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, kind, x, ldx, rows, dim, scale,
+                     offset);
   CE_HIP(hipGetLastError());
   return CE_GPU_OK;
+}
+
+int launch_rowop(hipStream_t s, const RowOp &op, float *x, int ldx, int rows) {
+  return launch_rowop_raw(s, op.kind, op.dim, op.scale.as<float>(), op.offset.as<float>(), x, ldx, rows);
 }
 
 }  // namespace catears

@@ -25,7 +25,8 @@ ABI = [
     "ce_gpu_fbank_num_frames", "ce_gpu_plan_create", "ce_gpu_plan_info",
     "ce_gpu_plan_frame_offsets", "ce_gpu_plan_destroy", "ce_gpu_fbank", "ce_gpu_cmvn",
     "ce_gpu_am_forward", "ce_gpu_score", "ce_gpu_sgemm", "ce_gpu_quantize",
-    "ce_gpu_gemm_u8u8f32", "ce_gpu_gemm_u8u8i32",
+    "ce_gpu_gemm_u8u8f32", "ce_gpu_gemm_u8u8i32", "ce_gpu_model_load_mem",
+    "ce_gpu_nnet_propagate", "ce_gpu_linear", "ce_gpu_splice", "ce_gpu_rowwise",
 ]
 
 _lib = None
@@ -75,6 +76,11 @@ def lib():
         "ce_gpu_quantize": (ci, [vp, vp, i64, vp, vp]),
         "ce_gpu_gemm_u8u8f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp]),
         "ce_gpu_gemm_u8u8i32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp]),
+        "ce_gpu_model_load_mem": (ci, [vp, vp, i64, vp, ci, ci, ci, pp]),
+        "ce_gpu_nnet_propagate": (ci, [vp, vp, vp, ci, ci, ci, vp]),
+        "ce_gpu_linear": (ci, [vp, ci, ci, ci, vp, ci, vp, ci, vp, vp, ci]),
+        "ce_gpu_splice": (ci, [vp, ci, ci, vp, ci, ctypes.POINTER(ctypes.c_int32), ci, vp]),
+        "ce_gpu_rowwise": (ci, [vp, ci, ci, ci, vp, ci, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -142,10 +148,20 @@ class Context:
 
 
 class Model:
-    def __init__(self, ctx, config_path=None, nnet=None, prior=None, left=None, right=None):
+    """config_path | (nnet, prior, left, right) files | image= NN02 bytes
+    (+ optional prior probabilities, left/right default to the network's)."""
+
+    def __init__(self, ctx, config_path=None, nnet=None, prior=None, left=None, right=None, image=None):
         h = ctypes.c_void_p()
         if config_path is not None:
             check(lib().ce_gpu_model_load_config(ctx.h, config_path.encode(), ctypes.byref(h)))
+        elif image is not None:
+            pr = None if prior is None else np.ascontiguousarray(prior, np.float32)
+            buf = ctypes.create_string_buffer(bytes(image), len(image))
+            check(lib().ce_gpu_model_load_mem(
+                ctx.h, buf, len(image), None if pr is None else pr.ctypes.data_as(ctypes.c_void_p),
+                0 if pr is None else pr.size, -1 if left is None else left, -1 if right is None else right,
+                ctypes.byref(h)))
         else:
             check(lib().ce_gpu_model_load(ctx.h, nnet.encode(), prior.encode(), left, right,
                                           ctypes.byref(h)))
@@ -241,6 +257,17 @@ def score(ctx, model, plan, pcm, global_stats=None, ws=None, out=None):
     if out is None:
         out = torch.empty((plan.total_frames, model.num_pdfs), dtype=torch.float32, device=pcm.device)
     check(lib().ce_gpu_score(ctx.h, model.h, plan.h, _ptr(pcm), _ptr(global_stats), _ptr(ws), _ptr(out)))
+    return out
+
+
+def nnet_propagate(ctx, model, x, subtract_prior=False, out=None):
+    """Nnet::Propagate on one padded block (+ the AM's prior subtraction)."""
+    import torch
+    net_l, net_r = model.left, model.right
+    rows = x.shape[0]
+    if out is None:
+        out = torch.empty((max(rows - net_l - net_r, 0), model.num_pdfs), dtype=torch.float32, device=x.device)
+    check(lib().ce_gpu_nnet_propagate(ctx.h, model.h, _ptr(x), rows, x.stride(0), int(subtract_prior), _ptr(out)))
     return out
 
 

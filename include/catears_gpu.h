@@ -113,6 +113,13 @@ int ce_gpu_model_info(const ce_gpu_model *m, int *left_context, int *right_conte
 int ce_gpu_model_tid2pdf(const ce_gpu_model *m, int32_t *h_out, int capacity, int *size);
 int ce_gpu_model_destroy(ce_gpu_model *m);
 
+/* Nnet::Read (src/nnet.cc:273-293) from an in-memory NN02 image (the bytes
+ * Nnet::Read consumes).  h_prior (prior_dim probabilities, log taken as in
+ * src/am.cc:40-44) may be NULL for a bare Nnet.  left/right_context < 0 take
+ * the context from the network's Narrow layers; otherwise they must agree. */
+int ce_gpu_model_load_mem(ce_gpu_ctx *ctx, const void *nnet, int64_t nbytes, const float *h_prior,
+                          int prior_dim, int left_context, int right_context, ce_gpu_model **out);
+
 /* --------------------------------------------------------------- plan --- */
 
 /* Frames of one utterance of n samples: 0 if n < 400 else 1 + (n - 400) / 160
@@ -159,6 +166,16 @@ int ce_gpu_cmvn(ce_gpu_ctx *ctx, const ce_gpu_plan *p, const float *d_global_sta
 int ce_gpu_am_forward(ce_gpu_ctx *ctx, const ce_gpu_model *m, const ce_gpu_plan *p,
                       const float *d_feats, float *d_loglik);
 
+/* Nnet::Propagate (src/nnet.cc:295-307) on one block of rows already padded
+ * by the caller, optionally followed by AcousticModel::ComputeBatch's prior
+ * subtraction (src/am.cc:104-112): d_in is rows x input_dim (row stride ld_in
+ * floats), d_out receives (rows - L - R) x num_pdfs where L, R are the rows the
+ * network's Narrow layers drop.  rows must exceed L + R (the reference's
+ * Narrow passes shorter blocks through unchanged, src/nnet.cc:186-189; that
+ * degenerate case is CE_GPU_EINVAL here). */
+int ce_gpu_nnet_propagate(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *d_in, int rows, int ld_in,
+                          int subtract_prior, float *d_out);
+
 /* The whole path: fbank -> (CMVN if d_global_stats != NULL) -> nnet -> - log
  * prior.  d_feats_ws must hold 2 x total_frames x 40 floats (features and
  * normalised features). */
@@ -196,6 +213,33 @@ int ce_gpu_gemm_u8u8f32(ce_gpu_ctx *ctx, int m, int n, int k, const uint8_t *d_a
 int ce_gpu_gemm_u8u8i32(ce_gpu_ctx *ctx, int m, int n, int k, const uint8_t *d_a,
                         const void *d_params_a, const uint8_t *d_b, const void *d_params_b,
                         int32_t *d_c);
+
+/* ------------------------------------------------------ layer primitives --- */
+/* Single layers for Layer::Propagate (src/nnet.h:34-42) outside a fused
+ * program.  All enqueue on the context's stream. */
+
+/* LinearLayer::Propagate (src/nnet.cc:22-43): out = in * W + b, W in_dim x
+ * out_dim row-major (MAT0 layout) with row stride ld_w; d_b may be NULL. */
+int ce_gpu_linear(ce_gpu_ctx *ctx, int rows, int in_dim, int out_dim, const float *d_in, int ld_in,
+                  const float *d_w, int ld_w, const float *d_b, float *d_out, int ld_out);
+
+/* SpliceLayer::Propagate (src/nnet.cc:50-95): out (rows x dim*n_idx, dense)
+ * row t = concat_s in[clamp(t + h_idx[s], 0, rows - 1)].  h_idx is host
+ * memory, 1 <= n_idx <= CE_GPU_MAX_SPLICE. */
+#define CE_GPU_MAX_SPLICE 32
+int ce_gpu_splice(ce_gpu_ctx *ctx, int rows, int dim, const float *d_in, int ld_in, const int32_t *h_idx,
+                  int n_idx, float *d_out);
+
+/* In-place per-row layers: ReLU (src/nnet.cc:149-160), BatchNorm (x*scale
+ * then +offset, :106-123), LogSoftmax (:137-146), Softmax, Normalize
+ * (:163-178).  d_scale/d_offset only for BatchNorm. */
+#define CE_GPU_ROW_RELU 0
+#define CE_GPU_ROW_BATCHNORM 1
+#define CE_GPU_ROW_LOGSOFTMAX 2
+#define CE_GPU_ROW_SOFTMAX 3
+#define CE_GPU_ROW_NORMALIZE 4
+int ce_gpu_rowwise(ce_gpu_ctx *ctx, int op, int rows, int dim, float *d_x, int ld, const float *d_scale,
+                   const float *d_offset);
 
 #ifdef __cplusplus
 }  /* extern "C" */

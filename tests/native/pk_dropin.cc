@@ -1,0 +1,226 @@
+// pk_dropin.cc -- test driver for the drop-in pocketkaldi classes
+// (catears_amd/host).  It uses them exactly the way the reference's callers
+// do -- ce_stt_process feeds Fbank::Process with arbitrary sample chunks and
+// AcousticModel::Process one frame at a time (src/ce_stt.cc:295-362); the
+// reference tests call Nnet::Propagate, CMVN::GetFrame, MatMat, Quantize and
+// MatMat_U8U8F32 directly -- and writes raw little-endian results for
+// tests/test_dropin.py to compare with the oracle.
+//
+//   pk_dropin fbank  <pcm.f32> <chunk> <out.f32>
+//   pk_dropin cmvn   <feats.f32> <rows> <stats.vec0> <out.f32>
+//   pk_dropin am     <am.conf> <feats.f32> <rows> <out.f32>      (per-frame Process + EndOfStream)
+//   pk_dropin nnet   <nnet.nn02> <in.f32> <rows> <cols> <out.f32> (Nnet::Read + Propagate)
+//   pk_dropin layer  <nnet.nn02> <in.f32> <rows> <cols> <out.f32> (Layer::Propagate of each layer, chained)
+//   pk_dropin matmat <m> <n> <k> <a.f32> <b.f32> <out.f32>
+//   pk_dropin quant  <rows> <cols> <in.f32> <out.u8> <params.bin>
+//   pk_dropin gemmu8 <m> <n> <k> <a.u8> <b.u8> <params_a.bin> <params_b.bin> <out.f32>
+// Every output file starts with two int32: rows, cols.
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "am.h"
+#include "cmvn.h"
+#include "configuration.h"
+#include "fbank.h"
+#include "matrix.h"
+#include "nnet.h"
+
+using namespace pocketkaldi;
+
+template <typename T>
+static std::vector<T> load(const char *path) {
+  FILE *f = fopen(path, "rb");
+  if (!f) {
+    fprintf(stderr, "cannot open %s\n", path);
+    exit(2);
+  }
+  fseek(f, 0, SEEK_END);
+  const long n = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  std::vector<T> v(n / sizeof(T));
+  if (n && fread(v.data(), 1, n, f) != (size_t)n) exit(2);
+  fclose(f);
+  return v;
+}
+
+template <typename T>
+static void save(const char *path, const T *data, int rows, int cols, int stride) {
+  FILE *f = fopen(path, "wb");
+  if (!f) exit(2);
+  int32_t hdr[2] = {rows, cols};
+  fwrite(hdr, 4, 2, f);
+  for (int r = 0; r < rows; ++r) fwrite(data + (size_t)r * stride, sizeof(T), cols, f);
+  fclose(f);
+}
+
+static void fill(Matrix<float> *m, const std::vector<float> &v, int rows, int cols) {
+  m->Resize(rows, cols, Matrix<float>::kUndefined);
+  for (int r = 0; r < rows; ++r) memcpy(m->Row(r).Data(), &v[(size_t)r * cols], sizeof(float) * cols);
+}
+
+static void append_rows(std::vector<float> *all, const Matrix<float> &m, int *cols) {
+  for (int r = 0; r < m.NumRows(); ++r) {
+    const SubVector<float> row = m.Row(r);
+    all->insert(all->end(), row.Data(), row.Data() + row.Dim());
+    *cols = row.Dim();
+  }
+}
+
+static int die(const Status &st) {
+  fprintf(stderr, "%s\n", st.what().c_str());
+  return 3;
+}
+
+int main(int argc, char **argv) {
+  if (argc < 2) return 1;
+  const std::string mode = argv[1];
+  if (mode == "fbank" && argc == 5) {
+    const std::vector<float> pcm = load<float>(argv[2]);
+    const int chunk = atoi(argv[3]);
+    Fbank fbank;
+    Fbank::Instance inst;
+    std::vector<float> all;
+    int cols = 40;
+    for (size_t at = 0; at < pcm.size(); at += chunk) {
+      const int n = (int)std::min<size_t>(chunk, pcm.size() - at);
+      Vector<float> wave(n, Vector<float>::kUndefined);
+      memcpy(wave.Data(), &pcm[at], sizeof(float) * n);
+      Matrix<float> feats;
+      fbank.Process(&inst, wave, &feats);
+      append_rows(&all, feats, &cols);
+    }
+    save(argv[4], all.data(), (int)(all.size() / 40), 40, 40);
+    return 0;
+  }
+  if (mode == "cmvn" && argc == 6) {
+    const int rows = atoi(argv[3]);
+    Matrix<float> raw;
+    fill(&raw, load<float>(argv[2]), rows, 40);
+    Vector<float> stats;
+    util::ReadableFile fd;
+    Status st = fd.Open(argv[4]);
+    if (st.ok()) st = stats.Read(&fd);
+    if (!st.ok()) return die(st);
+    CMVN cmvn(stats, raw);
+    Matrix<float> out(rows, 40);
+    for (int t = 0; t < rows; ++t) {
+      SubVector<float> row = out.Row(t);
+      cmvn.GetFrame(t, &row);
+    }
+    save(argv[5], out.Data(), rows, 40, out.Stride());
+    return 0;
+  }
+  if (mode == "am" && argc == 6) {
+    Configuration conf;
+    Status st = conf.Read(argv[2]);
+    AcousticModel am;
+    if (st.ok()) st = am.Read(conf);
+    if (!st.ok()) return die(st);
+    const int rows = atoi(argv[4]);
+    const std::vector<float> feats = load<float>(argv[3]);
+    const int dim = rows ? (int)(feats.size() / rows) : 0;
+    AcousticModel::Instance inst;
+    std::vector<float> all;
+    int cols = am.num_pdfs();
+    Matrix<float> log_prob;
+    for (int t = 0; t < rows; ++t) {
+      SubVector<float> frame(const_cast<float *>(&feats[(size_t)t * dim]), dim);
+      am.Process(&inst, frame, &log_prob);
+      append_rows(&all, log_prob, &cols);
+    }
+    am.EndOfStream(&inst, &log_prob);
+    append_rows(&all, log_prob, &cols);
+    save(argv[5], all.data(), cols ? (int)(all.size() / cols) : 0, cols, cols);
+    return 0;
+  }
+  if ((mode == "nnet" || mode == "layer") && argc == 7) {
+    Nnet nnet;
+    util::ReadableFile fd;
+    Status st = fd.Open(argv[2]);
+    if (st.ok()) st = nnet.Read(&fd);
+    if (!st.ok()) return die(st);
+    const int rows = atoi(argv[4]), cols = atoi(argv[5]);
+    Matrix<float> in, out;
+    fill(&in, load<float>(argv[3]), rows, cols);
+    if (mode == "nnet") {
+      nnet.Propagate(in, &out);
+    } else {
+      // the same network, one host-level Layer::Propagate per layer
+      util::ReadableFile f2;
+      st = f2.Open(argv[2]);
+      if (!st.ok()) return die(st);
+      st = f2.ReadAndVerifyString(PK_NNET_SECTION);
+      int32_t l, r, n;
+      f2.ReadValue(&l), f2.ReadValue(&r), f2.ReadValue(&n);
+      Matrix<float> cur;
+      cur.Resize(rows, cols);
+      cur.CopyFromMat(in);
+      for (int i = 0; i < n; ++i) {
+        st = f2.ReadAndVerifyString(PK_NNET_LAYER_SECTION);
+        int32_t id = -1;
+        f2.ReadValue(&id);
+        std::unique_ptr<Layer> layer;
+        switch (id) {
+          case Layer::kLinear: layer.reset(new LinearLayer()); break;
+          case Layer::kReLU: layer.reset(new ReLULayer()); break;
+          case Layer::kNormalize: layer.reset(new NormalizeLayer()); break;
+          case Layer::kSoftmax: layer.reset(new SoftmaxLayer()); break;
+          case Layer::kSplice: layer.reset(new SpliceLayer()); break;
+          case Layer::kBatchNorm: layer.reset(new BatchNormLayer()); break;
+          case Layer::kLogSoftmax: layer.reset(new LogSoftmaxLayer()); break;
+          case Layer::kNarrow: layer.reset(new NarrowLayer()); break;
+          default: return 4;
+        }
+        st = layer->Read(&f2);
+        if (!st.ok()) return die(st);
+        Matrix<float> next;
+        layer->Propagate(cur, &next);
+        cur.Swap(&next);
+      }
+      out.Swap(&cur);
+    }
+    save(argv[6], out.Data(), out.NumRows(), out.NumCols(), out.Stride());
+    return 0;
+  }
+  if (mode == "matmat" && argc == 8) {
+    const int m = atoi(argv[2]), n = atoi(argv[3]), k = atoi(argv[4]);
+    Matrix<float> A, B, C(m, n);
+    fill(&A, load<float>(argv[5]), m, k);
+    fill(&B, load<float>(argv[6]), k, n);
+    MatMat(A, B, &C);
+    save(argv[7], C.Data(), m, n, C.Stride());
+    return 0;
+  }
+  if (mode == "quant" && argc == 7) {
+    const int rows = atoi(argv[2]), cols = atoi(argv[3]);
+    Matrix<float> X;
+    fill(&X, load<float>(argv[4]), rows, cols);
+    Matrix<uint8_t> Q;
+    QuantizationParams qp;
+    Quantize(X, &Q, &qp);
+    save(argv[5], Q.Data(), rows, cols, Q.Stride());
+    FILE *f = fopen(argv[6], "wb");
+    fwrite(&qp, sizeof(qp), 1, f);
+    fclose(f);
+    return 0;
+  }
+  if (mode == "gemmu8" && argc == 10) {
+    const int m = atoi(argv[2]), n = atoi(argv[3]), k = atoi(argv[4]);
+    const std::vector<uint8_t> a = load<uint8_t>(argv[5]), b = load<uint8_t>(argv[6]);
+    const std::vector<QuantizationParams> pa = load<QuantizationParams>(argv[7]),
+                                          pb = load<QuantizationParams>(argv[8]);
+    Matrix<uint8_t> A(m, k), B(k, n);
+    memcpy(A.Data(), a.data(), a.size());
+    memcpy(B.Data(), b.data(), b.size());
+    Matrix<float> C(m, n);
+    MatMat_U8U8F32(A, pa[0], B, pb[0], &C);
+    save(argv[9], C.Data(), m, n, C.Stride());
+    return 0;
+  }
+  fprintf(stderr, "bad arguments\n");
+  return 1;
+}
