@@ -46,17 +46,23 @@ def parse():
     ap.add_argument("--model", default="tdnn-s")
     ap.add_argument("--no-cmvn", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
-    ap.add_argument("--cpu-utts", type=int, default=32, help="utterances in the CPU baseline sample")
+    ap.add_argument("--cpu-utts", type=int, default=32, help="distinct utterances in the CPU baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="minimum wall time of the CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the HIP-event kernel timing")
     ap.add_argument("--serial", action="store_true", help="one stream: no front/back stage overlap")
+    ap.add_argument("--back-streams", type=int, default=3,
+                    help="nnet streams; consecutive batches alternate between them so one batch's "
+                         "wave-quantisation tail overlaps the next batch's layers")
     return ap.parse_args()
 
 
-def cpu_baseline(conf, n_utts, seconds, threads):
+def cpu_baseline(conf, n_utts, seconds, threads, min_wall):
     """Oracle restatement ('port') of fbank -> CMVN -> nnet -> -log prior on the
     host cores: one utterance per worker thread, single-threaded OpenBLAS sgemm
-    (numpy) inside each worker, like the reference's cblas_sgemm path."""
+    (numpy) inside each worker, like the reference's cblas_sgemm path.  Passes
+    over the n_utts distinct utterances repeat until min_wall seconds of CPU
+    work have run (a bounded sample of the same workload)."""
     from concurrent.futures import ThreadPoolExecutor
 
     from catears_amd import formats, synth
@@ -78,14 +84,43 @@ def cpu_baseline(conf, n_utts, seconds, threads):
     ctxm = threadpool_limits(limits=1) if threadpool_limits else None
     try:
         one(waves[0][:16000])  # warm up
+        frames, passes = 0, 0
         t0 = time.perf_counter()
         with ThreadPoolExecutor(threads) as ex:
-            frames = sum(ex.map(one, waves))
+            while True:
+                frames += sum(ex.map(one, waves))
+                passes += 1
+                if time.perf_counter() - t0 >= min_wall or passes >= 200:
+                    break
         dt = time.perf_counter() - t0
     finally:
         if ctxm is not None:
             ctxm.__exit__(None, None, None)
-    return frames / dt, frames, dt
+    return frames / dt, frames, dt, passes
+
+
+ROOFLINE_KERNEL = "gemm_f32_pipe2_kernel<catears::Cfg<64, 128, 32, 2, 2>, true, false, false>"
+
+
+def gemm_algorithmic_bytes(rows, layers=((3072, 1024),) * 4 + ((1024, 1024), (1024, 3456))):
+    """fp32 A (rows x K) + W (K x N) + C (rows x N) bytes of TDNN-S layers 2-7,
+    per launch on average (one launch per layer)."""
+    return sum(4 * (rows * k + k * n + rows * n) for k, n in layers) / len(layers)
+
+
+def pmc_traffic(kernel):
+    """Per-launch HBM bytes of `kernel` from the newest committed PMC summary
+    (tools/pmc_traffic.py over rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
+    of this same bench); None if there is none."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    data = json.load(open(files[-1]))
+    for name, v in data.get("kernels", {}).items():
+        if name.endswith(kernel):
+            return v["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+    return None, None
 
 
 def main():
@@ -113,12 +148,16 @@ def main():
         dist.barrier()
     conf = synth.write_model(mdir, args.model)  # no-op once written
 
-    # Two-stage software pipeline on two HIP streams: the front stage (fbank +
-    # CMVN, a handful of waves) of batch i+1 runs beside the nnet GEMMs of
-    # batch i.  Each batch is still scored end to end inside the timed region.
-    back = torch.cuda.current_stream()
-    front = torch.cuda.Stream() if not args.serial else back
-    ctx = gpu.Context(local, back)
+    # Software pipeline: a front stream runs fbank + CMVN of batch i+1 (a
+    # handful of waves) beside the nnet GEMMs of batch i, and the nnet work of
+    # consecutive batches alternates between `back_streams` streams so the
+    # partial last wave of one batch's layers overlaps the next batch's.
+    # Every batch is still scored end to end inside the timed region.
+    NB = 1 if args.serial else max(1, args.back_streams)
+    backs = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(NB - 1)]
+    front = torch.cuda.Stream() if not args.serial else backs[0]
+    ctxs = [gpu.Context(local, b) for b in backs]
+    ctx = ctxs[0]
     ctx_f = gpu.Context(local, front) if not args.serial else ctx
     model = gpu.Model(ctx, conf)
     n_samp = int(16000 * args.seconds)
@@ -131,20 +170,22 @@ def main():
     pool = max(args.pool, U)
     pcm = torch.from_numpy(np.stack([synth.pcm(rank * 100003 + i, n_samp) for i in range(pool)])).cuda()
     gstats = None if args.no_cmvn else torch.from_numpy(synth.cmvn_stats_synthetic()).cuda()
-    raw = [torch.empty((frames_per_step, 40), dtype=torch.float32, device="cuda") for _ in range(2)]
-    norm = [torch.empty_like(raw[0]) for _ in range(2)] if gstats is not None else raw
-    ready = [torch.cuda.Event() for _ in range(2)]
-    free = [torch.cuda.Event() for _ in range(2)]
-    nbuf = 3
+    F = NB + 1  # feature slots: one being filled while NB are being scored
+    raw = [torch.empty((frames_per_step, 40), dtype=torch.float32, device="cuda") for _ in range(F)]
+    norm = [torch.empty_like(raw[0]) for _ in range(F)] if gstats is not None else raw
+    ready = [torch.cuda.Event() for _ in range(F)]
+    free = [torch.cuda.Event() for _ in range(F)]
+    nbuf = max(3, NB + 1)
     outs = [torch.empty((frames_per_step, model.num_pdfs), dtype=torch.float32, device="cuda")
             for _ in range(nbuf)]
+    done = [None] * nbuf  # event: the batch that last wrote outs[o] has finished
     gather = world > 1 and not args.no_gather
     gat = LoglikGather(outs[0].shape, torch.float32, "cuda", depth=nbuf) if gather else None
     checksum = torch.zeros((), dtype=torch.float64, device="cuda")
 
     def front_stage(i):
-        slot = i % 2
-        front.wait_event(free[slot])  # batch i-2 has finished reading this slot
+        slot = i % F
+        front.wait_event(free[slot])  # the batch F steps ago has finished reading this slot
         first = (i * U) % (pool - U + 1)
         src = pcm[first:first + U].reshape(-1)
         gpu.fbank(ctx_f, plan, src, raw[slot])
@@ -153,13 +194,23 @@ def main():
         ready[slot].record(front)
 
     def back_stage(i):
-        slot, o = i % 2, i % nbuf
+        slot, o, b = i % F, i % nbuf, i % NB
+        stream = backs[b]
         if gat is not None:
             gat.wait_slot(o)  # the gather from nbuf steps ago has read outs[o]
-        back.wait_event(ready[slot])
-        gpu.am_forward(ctx, model, plan, norm[slot], outs[o])
-        free[slot].record(back)
+            # the collective runs on the default (first) stream: order the write after it
+            if b:
+                stream.wait_stream(backs[0])
+        if done[o] is not None:
+            stream.wait_event(done[o])  # the batch nbuf steps ago (maybe another stream) wrote outs[o]
+        stream.wait_event(ready[slot])
+        gpu.am_forward(ctxs[b], model, plan, norm[slot], outs[o])
+        free[slot].record(stream)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        done[o] = ev
         if gat is not None:
+            backs[0].wait_event(ev)
             assert gat.submit(outs[o]) == o
 
     def run(first, count):
@@ -174,8 +225,9 @@ def main():
         gat.drain()
     torch.cuda.synchronize()
     if not args.no_profile:
-        ctx.profile(True)
-        ctx_f.profile(True)
+        gpu.profile_anchor(local, backs[0])
+        for c in set(ctxs + [ctx_f]):
+            c.profile(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -197,12 +249,16 @@ def main():
 
     prof = {}
     if not args.no_profile:
-        ctx.profile(False)
-        ctx_f.profile(False)
-        for name, c, cls in (("gemm", ctx, ctx.PROF_GEMM), ("gemm_gather", ctx, ctx.PROF_GEMM_GATHER),
-                             ("fbank", ctx_f, ctx.PROF_FBANK), ("cmvn", ctx_f, ctx.PROF_CMVN),
-                             ("finalize", ctx, ctx.PROF_FINALIZE)):
-            prof[name] = c.profile_read(cls)
+        for c in set(ctxs + [ctx_f]):
+            c.profile(False)
+        for name, cs, cls in (("gemm", ctxs, ctx.PROF_GEMM), ("gemm_gather", ctxs, ctx.PROF_GEMM_GATHER),
+                              ("fbank", [ctx_f], ctx.PROF_FBANK), ("cmvn", [ctx_f], ctx.PROF_CMVN),
+                              ("finalize", ctxs, ctx.PROF_FINALIZE)):
+            iv = []
+            for c in cs:
+                iv += c.profile_intervals(cls)
+            # (sum of launch durations, launches, wall time the class was on the device)
+            prof[name] = (sum(b - a for a, b in iv), len(iv), gpu.union_ms(iv))
 
     total_frames = frames_per_step * args.steps * world
     value = total_frames / elapsed
@@ -215,20 +271,29 @@ def main():
     roofline = None
     stages = {}
     if prof:
-        ms, n = prof["gemm"]
+        ms, n, busy = prof["gemm"]
         if n:
+            # With several nnet streams, launches of this kernel overlap each
+            # other; a launch's own duration then includes time shared with
+            # its neighbour.  `achieved` is therefore the algorithmic FLOPs of
+            # all launches over the wall time during which at least one was
+            # running (the union of their intervals) -- with one stream this
+            # is exactly FLOPs per launch / average launch duration.
             flops_per_launch = frames_per_step * FLOPS_PER_FRAME_FAST / (n / args.steps)
-            avg_ms = ms / n
-            achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
+            achieved = flops_per_launch * n / (busy * 1e-3) / 1e12
+            traffic, src = pmc_traffic(ROOFLINE_KERNEL)
             roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": MFMA_F32_PEAK_TFLOPS,
                         "unit": "TFLOP/s", "frac": round(achieved / MFMA_F32_PEAK_TFLOPS, 4),
-                        "traffic": None, "kernel": "gemm_f32_pipe2_kernel<Cfg<64,128,32,2,2>,true,false,false> (TDNN layers 2-7)",
-                        "launches": n, "avg_launch_ms": round(avg_ms, 4),
-                        "flops_per_launch": flops_per_launch}
-        for name, (ms, n) in prof.items():
+                        "traffic": traffic, "traffic_source": src,
+                        "kernel": ROOFLINE_KERNEL + " (TDNN-S layers 2-7)",
+                        "launches": n, "avg_launch_ms": round(ms / n, 4), "busy_ms": round(busy, 3),
+                        "effective_ms_per_launch": round(busy / n, 4),
+                        "flops_per_launch": flops_per_launch,
+                        "algorithmic_bytes_per_launch": gemm_algorithmic_bytes(plan.max_chunk_rows)}
+        for name, (ms, n, busy) in prof.items():
             if n:
-                stages[name] = {"launches": n, "avg_ms": round(ms / n, 4),
-                                "share_of_step": round(ms / (elapsed * 1e3), 4)}
+                stages[name] = {"launches": n, "avg_ms": round(ms / n, 4), "busy_ms": round(busy, 3),
+                                "share_of_step": round(busy / (elapsed * 1e3), 4)}
         if "fbank" in stages:
             fb_bytes = 4 * U * n_samp + 4 * 40 * frames_per_step  # PCM read once + features written
             stages["fbank"]["hbm_GBs"] = round(fb_bytes / (stages["fbank"]["avg_ms"] * 1e-3) / 1e9, 1)
@@ -237,10 +302,11 @@ def main():
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
-        v, fr, dt = cpu_baseline(conf, args.cpu_utts, args.seconds, threads)
+        v, fr, dt, passes = cpu_baseline(conf, args.cpu_utts, args.seconds, threads, args.cpu_seconds)
         cpu = {"value": round(v, 1), "unit": "frames/s", "cores": threads, "kind": "port",
-               "sample": f"{args.cpu_utts} x {args.seconds:g} s utterances ({fr} frames, {dt:.1f} s wall): "
-                         f"oracle fbank+CMVN (C) + TDNN-S with single-threaded OpenBLAS sgemm per worker"}
+               "sample": f"{passes} passes over {args.cpu_utts} x {args.seconds:g} s utterances ({fr} frames, "
+                         f"{dt:.1f} s wall, {threads} worker threads): oracle fbank+CMVN (C) + TDNN-S with "
+                         f"single-threaded OpenBLAS sgemm per worker"}
 
     line = {
         "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world,
@@ -252,7 +318,7 @@ def main():
                                ("" if not gather else "; C4 RCCL gather of log-likelihoods to rank 0"),
                    "frames_per_step_per_gpu": frames_per_step, "packed_rows": plan.max_chunk_rows,
                    "cmvn": not args.no_cmvn, "parallelism": f"utterance shard x{world}",
-                   "streams": 1 if args.serial else 2,
+                   "streams": 1 if args.serial else 1 + NB,
                    "gather": gather},
         "roofline": roofline, "cpu_baseline": cpu, "stages": stages,
         "end_to_end_mfma_frac": round(value / world * FLOPS_PER_FRAME / 1e12 / MFMA_F32_PEAK_TFLOPS, 4),

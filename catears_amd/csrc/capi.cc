@@ -560,6 +560,49 @@ int ce_gpu_ctx_profile_read(ce_gpu_ctx *ctx, int kernel_class, double *total_ms,
   return CE_GPU_OK;
 }
 
+static hipEvent_t g_anchor[64];
+
+int ce_gpu_profile_anchor(int device, void *stream) {
+  if (device < 0 || device >= 64) return fail(CE_GPU_EINVAL, "bad device");
+  CE_HIP(hipSetDevice(device));
+  if (!g_anchor[device]) CE_HIP(hipEventCreate(&g_anchor[device]));
+  CE_HIP(hipEventRecord(g_anchor[device], static_cast<hipStream_t>(stream)));
+  return CE_GPU_OK;
+}
+
+int ce_gpu_ctx_profile_intervals(ce_gpu_ctx *ctx, int kernel_class, double *h_start_ms, double *h_end_ms,
+                                 int capacity, int *count) {
+  if (!ctx || !count || kernel_class < 0 || kernel_class >= CE_GPU_PROF_CLASSES)
+    return fail(CE_GPU_EINVAL, "bad argument");
+  hipEvent_t anchor = ctx->device < 64 ? g_anchor[ctx->device] : nullptr;
+  if (!anchor) return fail(CE_GPU_EINVAL, "no anchor recorded (ce_gpu_profile_anchor)");
+  CE_HIP(hipStreamSynchronize(ctx->stream));
+  CE_HIP(hipEventSynchronize(anchor));
+  int n = 0;
+  for (const ce_gpu_ctx::Timed &t : ctx->timed) n += t.cls == kernel_class;
+  *count = n;
+  if (n > capacity || (n > 0 && (!h_start_ms || !h_end_ms)))
+    return fail(CE_GPU_EINVAL, fmt("capacity %d < %d launches", capacity, n));
+  std::vector<ce_gpu_ctx::Timed> keep;
+  int i = 0;
+  for (const ce_gpu_ctx::Timed &t : ctx->timed) {
+    if (t.cls != kernel_class) {
+      keep.push_back(t);
+      continue;
+    }
+    float a = 0.0f, b = 0.0f;
+    CE_HIP(hipEventElapsedTime(&a, anchor, t.a));
+    CE_HIP(hipEventElapsedTime(&b, anchor, t.b));
+    h_start_ms[i] = a;
+    h_end_ms[i] = b;
+    ++i;
+    ctx->event_pool.push_back(t.a);
+    ctx->event_pool.push_back(t.b);
+  }
+  ctx->timed.swap(keep);
+  return CE_GPU_OK;
+}
+
 int ce_gpu_model_load(ce_gpu_ctx *ctx, const char *nnet_path, const char *prior_path, int left_context,
                       int right_context, ce_gpu_model **out) {
   if (!ctx || !nnet_path || !prior_path || !out) return fail(CE_GPU_EINVAL, "NULL argument");

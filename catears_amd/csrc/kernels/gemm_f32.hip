@@ -22,6 +22,7 @@
 // distinct 16-byte bank slots.  Two LDS stages; the next K-tile's global
 // loads are issued before the current tile's MFMAs.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "../internal.h"
 
@@ -44,6 +45,7 @@ struct KArgs {
   int post[4];
   int npost;
   int tiles_m, tiles_n;
+  int group;  // column tiles per tile group (tile_of)
 };
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
@@ -182,15 +184,23 @@ struct Stage {
   }
 };
 
-// XCD-aware tile order: blocks b and b+8 run on one XCD (round-robin
-// dispatch), so give each XCD a contiguous run of tiles in column-major tile
-// order -- the blocks of one XCD then share weight panels in its L2.  The
-// remap is bijective for any grid size (a speed choice, never correctness).
-__device__ __forceinline__ void tile_of(int b, int tiles_m, int tiles_n, int *tm, int *tn) {
+// XCD-aware tile order.  Blocks b, b+8, b+16, ... run on one XCD
+// (round-robin dispatch), so each XCD gets a contiguous run of a global tile
+// order, and that order walks compact 2-D blocks: groups of `group` column
+// tiles, row blocks inside a group, columns inside a row.  For the 3072 x 1024
+// layers at 64 x 128 tiles an XCD's 64 tiles are then a 16 x 4 block: it
+// fetches 16 A row panels and 4 weight panels into its L2 (~19 MB) instead
+// of all of A (51 MB) under a plain column-major order.  Bijective for any
+// grid (a speed choice, never correctness).
+__device__ __forceinline__ void tile_of(int b, int tiles_m, int tiles_n, int group, int *tm, int *tn) {
   const int nwg = tiles_m * tiles_n, q = nwg / 8, r = nwg % 8, xcd = b % 8;
   const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
-  *tn = t / tiles_m;
-  *tm = t - *tn * tiles_m;
+  const int per_group = group * tiles_m;
+  const int g = t / per_group, rem = t - g * per_group;
+  const int w = min(group, tiles_n - g * group);  // the last group may be narrower
+  const int rb = rem / w;
+  *tm = rb;
+  *tn = g * group + (rem - rb * w);
 }
 
 template <class C, bool A_FAST, bool B_NMAJOR, bool ROWMAP>
@@ -200,7 +210,7 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_kernel(KArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / C::WGN, wn = wave % C::WGN;
   int tm, tn;
-  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, &tm, &tn);
+  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int r = lane & 31, h = lane >> 5;
 
@@ -299,7 +309,7 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_pipe_kernel(KArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / C::WGN, wn = wave % C::WGN;
   int tm, tn;
-  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, &tm, &tn);
+  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int r = lane & 31, h = lane >> 5;
   const int a_off = (wm * TI * 32 + r) * LDT + 4 * h;
@@ -410,7 +420,7 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_pipe2_kernel(KArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / C::WGN, wn = wave % C::WGN;
   int tm, tn;
-  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, &tm, &tn);
+  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int r = lane & 31, h = lane >> 5;
   const int a_off = (wm * TI * 32 + r) * LDT + 4 * h;
@@ -627,6 +637,11 @@ int launch_gemm_f32(hipStream_t s, const GemmArgs &a) {
   }
   for (int i = 0; i < 4; ++i) p.post[i] = a.post[i];
   p.npost = a.npost;
+  static const int group_env = [] {
+    const char *e = getenv("CATEARS_GEMM_GROUP");
+    return e ? atoi(e) : 0;
+  }();
+  p.group = group_env > 0 ? group_env : 4;
   // fast A path: every K-tile inside one segment, float4-aligned rows
   const bool a_fast = (a.ldx % 4 == 0) && ((reinterpret_cast<uintptr_t>(a.x) & 15) == 0);
   if (!a.b_nmajor && (a.ldw % 4 != 0 || (reinterpret_cast<uintptr_t>(a.w) & 15) != 0))

@@ -27,6 +27,7 @@ ABI = [
     "ce_gpu_am_forward", "ce_gpu_score", "ce_gpu_sgemm", "ce_gpu_quantize",
     "ce_gpu_gemm_u8u8f32", "ce_gpu_gemm_u8u8i32", "ce_gpu_model_load_mem",
     "ce_gpu_nnet_propagate", "ce_gpu_linear", "ce_gpu_splice", "ce_gpu_rowwise",
+    "ce_gpu_profile_anchor", "ce_gpu_ctx_profile_intervals",
 ]
 
 _lib = None
@@ -76,6 +77,8 @@ def lib():
         "ce_gpu_quantize": (ci, [vp, vp, i64, vp, vp]),
         "ce_gpu_gemm_u8u8f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp]),
         "ce_gpu_gemm_u8u8i32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp]),
+        "ce_gpu_profile_anchor": (ci, [ci, vp]),
+        "ce_gpu_ctx_profile_intervals": (ci, [vp, ci, vp, vp, ci, pi]),
         "ce_gpu_model_load_mem": (ci, [vp, vp, i64, vp, ci, ci, ci, pp]),
         "ce_gpu_nnet_propagate": (ci, [vp, vp, vp, ci, ci, ci, vp]),
         "ce_gpu_linear": (ci, [vp, ci, ci, ci, vp, ci, vp, ci, vp, vp, ci]),
@@ -135,6 +138,18 @@ class Context:
         check(lib().ce_gpu_ctx_profile_read(self.h, cls, ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
 
+    def profile_intervals(self, cls):
+        """[(start_ms, end_ms)] after the last profile_anchor(), per launch of a class."""
+        n = ctypes.c_int()
+        rc = lib().ce_gpu_ctx_profile_intervals(self.h, cls, None, None, 0, ctypes.byref(n))
+        if rc != CE_GPU_OK and n.value == 0:
+            check(rc)
+        a = np.zeros(max(n.value, 1), np.float64)
+        b = np.zeros_like(a)
+        check(lib().ce_gpu_ctx_profile_intervals(self.h, cls, a.ctypes.data_as(ctypes.c_void_p),
+                                                 b.ctypes.data_as(ctypes.c_void_p), len(a), ctypes.byref(n)))
+        return list(zip(a[:n.value], b[:n.value]))
+
     def close(self):
         if getattr(self, "h", None):
             lib().ce_gpu_ctx_destroy(self.h)
@@ -190,6 +205,26 @@ class Model:
             self.close()
         except Exception:
             pass
+
+
+def profile_anchor(device, stream):
+    """Record the time origin for Context.profile_intervals on `stream`."""
+    check(lib().ce_gpu_profile_anchor(device, ctypes.c_void_p(stream.cuda_stream)))
+
+
+def union_ms(intervals):
+    """Wall time covered by a set of (start, end) intervals."""
+    total, cur_a, cur_b = 0.0, None, None
+    for a, b in sorted(intervals):
+        if cur_b is None or a > cur_b:
+            if cur_b is not None:
+                total += cur_b - cur_a
+            cur_a, cur_b = a, b
+        else:
+            cur_b = max(cur_b, b)
+    if cur_b is not None:
+        total += cur_b - cur_a
+    return total
 
 
 def num_frames(n_samples):

@@ -88,6 +88,15 @@ int ce_gpu_ctx_synchronize(ce_gpu_ctx *ctx);
 int ce_gpu_ctx_profile(ce_gpu_ctx *ctx, int enable);
 int ce_gpu_ctx_profile_read(ce_gpu_ctx *ctx, int kernel_class, double *total_ms, int64_t *launches);
 
+/* Per-launch intervals for kernels that overlap across streams: record a
+ * device-wide time origin on `stream` (before the launches of interest), then
+ * read each launch's [start, end] in ms after it.  Consumes the records like
+ * profile_read; fails with CE_GPU_EINVAL (and the needed *count) if capacity
+ * is too small. */
+int ce_gpu_profile_anchor(int device, void *stream);
+int ce_gpu_ctx_profile_intervals(ce_gpu_ctx *ctx, int kernel_class, double *h_start_ms, double *h_end_ms,
+                                 int capacity, int *count);
+
 /* -------------------------------------------------------------- model --- */
 
 /* AcousticModel::Read (src/am.cc:26-64): reads the key=value config (keys

@@ -1,0 +1,28 @@
+# One GPU session: parity tests, the bench line under rocprofv3 kernel-trace
+# stats (same command -> JSON + per-kernel durations), then the two PMC
+# passes that give roofline.traffic.  Usage: TAG=r01x bash tools/round_gpu.sh
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${TAG:-run}
+OUT="$R/gpurun_out/$TAG"
+mkdir -p "$OUT"
+cd "$R" || exit 1
+timeout -k 10 900 python -m pytest tests -q -m gpu -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1; rc=$?
+echo "pytest rc=$rc"; tail -8 "$OUT/pytest_gpu.log"
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+[ -n "$SKIP_BENCH" ] && exit 0
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
+    python "$R/bench.py" --steps ${STEPS:-50} --warmup 5 ${BENCH_ARGS} > "$OUT/bench.log" 2>&1; rc=$?
+echo "bench(rocprof) rc=$rc"; tail -2 "$OUT/bench.log"
+[ $rc -eq 0 ] || exit $rc
+[ -n "$SKIP_PMC" ] && exit 0
+i=0
+for grp in FETCH_SIZE WRITE_SIZE; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "gemm_f32|fbank|cmvn|finalize" \
+      --output-format csv -d "$OUT/pmc$i" -o run -- \
+      python "$R/bench.py" --steps 4 --warmup 1 --no-cpu-baseline --no-profile --serial \
+      > "$OUT/pmc$i.log" 2>&1 || { echo "pmc pass $i failed"; tail -20 "$OUT/pmc$i.log"; exit 1; }
+  echo "pmc pass $i ok: $grp"
+done
+python "$R/tools/pmc_traffic.py" "$OUT/pmc1" "$OUT/pmc2" "$OUT/pmc_traffic.json"
