@@ -99,7 +99,7 @@ def cpu_baseline(conf, n_utts, seconds, threads, min_wall):
     return frames / dt, frames, dt, passes
 
 
-ROOFLINE_KERNEL = "gemm_f32_pipe2_kernel<catears::Cfg<64, 128, 32, 2, 2>, true, false, false>"
+ROOFLINE_KERNEL = "gemm_f32_glds_kernel<catears::Cfg<128, 64, 32, 2, 2>, 2>"
 
 
 def gemm_algorithmic_bytes(rows, layers=((3072, 1024),) * 4 + ((1024, 1024), (1024, 3456))):

@@ -54,7 +54,8 @@ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? l
 template <int BM_, int BN_, int BK_, int WGM_, int WGN_>
 struct Cfg {
   static constexpr int BM = BM_, BN = BN_, BK = BK_, WGM = WGM_, WGN = WGN_;
-  static_assert(WGM * WGN == 4, "4 waves per block");
+  static constexpr int NW = WGM * WGN, NT = 64 * NW;  // waves / threads per block
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves per block (8: LDS-DMA kernel only)");
   static constexpr int LDT = BK + 4;                // padded LDS row (floats)
   static constexpr int TI = BM / WGM / 32, TJ = BN / WGN / 32;
   static constexpr int AV = BM * BK / 4 / 256;      // float4 of A per thread
@@ -70,6 +71,7 @@ struct Cfg {
 // wait vmcnt(0) on every staging load, serialising the prefetch.
 template <class C, bool A_FAST, bool B_NMAJOR, bool ROWMAP>
 struct Stage {
+  static_assert(C::NW == 4, "register staging assumes 256 threads");
   static constexpr int NA = A_FAST ? C::AV : 1, NAS = A_FAST ? 1 : C::AS;
   static constexpr int NB = B_NMAJOR ? 1 : C::BV, NBS = B_NMAJOR ? C::BS : 1;
   f32x4 a[NA];
@@ -590,10 +592,207 @@ using V2 = Cfg<128, 64, 32, 2, 2>;
 using V3 = Cfg<64, 128, 32, 2, 2>;
 using V4 = Cfg<128, 64, 64, 2, 2>;
 using V8 = Cfg<64, 64, 32, 2, 2>;
+using W0 = Cfg<128, 128, 32, 4, 2>;  // 8 waves, 32 x 64 each
+using W1 = Cfg<128, 128, 32, 2, 4>;  // 8 waves, 64 x 32 each
+using W2 = Cfg<64, 128, 64, 2, 2>;
+using W3 = Cfg<128, 128, 64, 4, 2>;
+using W4 = Cfg<64, 128, 32, 2, 4>;   // 8 waves, 32 x 32 each
+using W5 = Cfg<128, 64, 32, 4, 2>;   // 8 waves, 32 x 32 each
+using W6 = Cfg<64, 256, 32, 2, 4>;   // 8 waves, 32 x 64 each
 
-// Default: write-after-barrier pipeline on 64 x 128 tiles (measured best on
-// TDNN-S, tools/gemm_variants.sh); CATEARS_GEMM_VARIANT overrides for tuning.
-constexpr int kDefaultVariant = 13;
+
+// ---------------------------------------------------------------------------
+// LDS-DMA pipeline (glds): operands go global -> LDS with
+// global_load_lds_dwordx4 (no VGPR staging, no ds_write pass), three LDS
+// stages, one raw s_barrier per K-tile and a counted vmcnt that keeps the
+// next tile's DMAs in flight across it (CDNA guide: "Pipelining across
+// barriers").  Requires the fast A path (every K-tile inside one splice
+// segment) and K-major weights -- the TDNN layers after the first.
+//
+// An LDS-DMA writes 64 lanes x 16 B contiguously, so tiles are stored
+// unpadded (BK = 32 floats = 128 B per row, 8 rows per instruction) and the
+// bank spread comes from an XOR swizzle applied on the SOURCE address: chunk
+// c of row r lands at chunk c ^ ((r >> 1) & 7).  The 16 lanes of a
+// ds_read_b128 group (rows r..r+15 of one fragment, one chunk) then cover the
+// 16 distinct 16-B slots of the 256-B bank row.
+//
+// Synchronisation per K-tile kt (stage kt % 3):
+//   s_waitcnt vmcnt(this wave's DMAs for kt+1)  -> this wave's kt landed
+//   s_barrier                                    -> every wave's kt landed, and
+//                                                   every wave is past its reads
+//                                                   of stage (kt-1) % 3
+//   issue DMAs for kt+2 into stage (kt+2) % 3 == (kt-1) % 3   (WAR safe)
+//   ds_read + MFMA on stage kt % 3
+// All LDS is one __shared__ array and the loop holds no ordinary global
+// loads, so hipcc adds no vmcnt(0) of its own.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void glds16(const char *src, float *lds_dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                   (__attribute__((address_space(3))) void *)lds_dst, 16, 0, 0);
+}
+
+template <class C, int STAGES>
+__global__ __launch_bounds__(C::NT, 1) void gemm_f32_glds_kernel(KArgs p) {
+  constexpr int BM = C::BM, BN = C::BN, BK = C::BK, TI = C::TI, TJ = C::TJ, NW = C::NW;
+  static_assert(BK == 32 || BK == 64, "tile rows of 128 or 256 bytes");
+  static_assert(STAGES == 2 || STAGES == 3, "2 or 3 LDS stages");
+  constexpr int CPR = BK / 4;                          // 16-B chunks per tile row
+  constexpr int RB = 256 / (BK * 4);                   // tile rows per 256-B bank row
+  constexpr int RPI = 1024 / (BK * 4);                 // tile rows per DMA instruction
+  constexpr int NGA = BM * BK * 4 / 1024 / NW;         // DMA instructions per wave, A
+  constexpr int NGB = BN * BK * 4 / 1024 / NW;         // and B
+  constexpr int NG = NGA + NGB;
+  static_assert(NGA >= 1 && NGB >= 1, "tile too small for one DMA per wave");
+  constexpr int STAGE = (BM + BN) * BK;                // floats per stage
+  __shared__ __attribute__((aligned(1024))) float smem[STAGES * STAGE];
+  // chunk c of tile row `row` is stored at chunk c ^ swz(row)
+  auto swz = [](int row) { return (row / RB) & (CPR - 1); };
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / C::WGN, wn = wave % C::WGN;
+  int tm, tn;
+  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int r = lane & 31, h = lane >> 5;
+
+  // per-lane DMA source offsets (bytes from the tile's uniform base)
+  const int lrow = lane / CPR, lchunk = lane % CPR;
+  uint32_t boff[NGB];
+#pragma unroll
+  for (int j = 0; j < NGB; ++j) {
+    const int row = (wave * NGB + j) * RPI + lrow;
+    const int c = lchunk ^ swz(row);
+    boff[j] = (uint32_t)((min(n0 + row, p.n - 1) * p.ldw + 4 * c) * 4);
+  }
+  uint32_t aoff[NGA];
+  int cur_seg = -1;
+
+  auto issue = [&](int kt) {
+    const int k0 = kt * BK;
+    const int seg = k0 / p.din, col0 = k0 - seg * p.din;
+    if (seg != cur_seg) {
+      cur_seg = seg;
+      const int shift = (int)(signed char)(p.off_packed >> (8 * seg));
+#pragma unroll
+      for (int i = 0; i < NGA; ++i) {
+        const int row = (wave * NGA + i) * RPI + lrow;
+        const int c = lchunk ^ swz(row);
+        const int src = clampi(m0 + row + shift, 0, p.m - 1);
+        aoff[i] = (uint32_t)(src * p.ldx + 4 * c) * 4u;
+      }
+    }
+    float *st = smem + (kt % STAGES) * STAGE;
+    const char *abase = reinterpret_cast<const char *>(p.x) + (size_t)col0 * 4;
+    const char *bbase = reinterpret_cast<const char *>(p.w) + (size_t)k0 * 4;
+#pragma unroll
+    for (int i = 0; i < NGA; ++i) glds16(abase + aoff[i], st + (wave * NGA + i) * RPI * BK);
+#pragma unroll
+    for (int j = 0; j < NGB; ++j) glds16(bbase + boff[j], st + BM * BK + (wave * NGB + j) * RPI * BK);
+  };
+
+  // fragment addresses: row base + swizzled chunk of k-group g (fragment
+  // rows start at multiples of 32, so swz(row) == swz(r))
+  const int xr = swz(r) ^ h;  // chunk 2g + h  ->  (2g) ^ xr
+  const int a_row = (wm * TI * 32 + r) * BK, b_row = BM * BK + (wn * TJ * 32 + r) * BK;
+
+  f32x16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+  auto frag = [&](const float *st, int g, f32x4 *fa, f32x4 *fb) {
+    const int ch = ((2 * g) ^ xr) * 4;
+#pragma unroll
+    for (int i = 0; i < TI; ++i) fa[i] = *reinterpret_cast<const f32x4 *>(st + a_row + i * 32 * BK + ch);
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) fb[j] = *reinterpret_cast<const f32x4 *>(st + b_row + j * 32 * BK + ch);
+  };
+  auto mma = [&](const f32x4 *fa, const f32x4 *fb) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+  };
+
+  const int ktiles = p.kpad / BK;
+  issue(0);
+  if (STAGES == 3 && ktiles > 1) issue(1);
+  for (int kt = 0; kt < ktiles; ++kt) {
+    if (STAGES == 3 && kt + 1 < ktiles)
+      wait_vmcnt<NG>();  // leave tile kt+1's DMAs in flight
+    else
+      wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (kt + STAGES - 1 < ktiles) issue(kt + STAGES - 1);
+    const float *st = smem + (kt % STAGES) * STAGE;
+    f32x4 fa0[TI], fb0[TJ], fa1[TI], fb1[TJ];
+    frag(st, 0, fa0, fb0);
+#pragma unroll
+    for (int g = 0; g < BK / 8; ++g) {
+      if (g + 1 < BK / 8) frag(st, g + 1, (g & 1) ? fa0 : fa1, (g & 1) ? fb0 : fb1);
+      mma((g & 1) ? fa1 : fa0, (g & 1) ? fb1 : fb0);
+    }
+  }
+
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int col = n0 + wn * TJ * 32 + j * 32 + r;
+    if (col >= p.n) continue;
+    const float bias = p.bias ? p.bias[col] : 0.0f;
+    const float sc = p.bn_scale ? p.bn_scale[col] : 1.0f;
+    const float of = p.bn_offset ? p.bn_offset[col] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = m0 + wm * TI * 32 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (row >= p.m) continue;
+        float v = acc[i][j][e];
+        if (p.bias) v = v + bias;
+        for (int q = 0; q < p.npost; ++q) {
+          if (p.post[q] == kPostRelu) {
+            v = v < 0.0f ? 0.0f : v;
+          } else if (p.post[q] == kPostBatchNorm) {
+            v = v * sc;
+            v = v + of;
+          }
+        }
+        p.y[(int64_t)row * p.ldy + col] = v;
+      }
+    }
+  }
+}
+
+// glds for the layers it fits, pipe2 for the rest (first layer's gather,
+// N-major MatMat operands).
+template <class C, int STAGES = 3>
+int launch_glds(hipStream_t s, KArgs p, bool a_fast, bool b_nmajor, bool rm) {
+  if (!(a_fast && !b_nmajor && !rm && p.din % C::BK == 0 && p.kpad % C::BK == 0))
+    return launch_pipe2<V3>(s, p, a_fast, b_nmajor, rm);
+  p.tiles_n = (p.n + C::BN - 1) / C::BN;
+  p.tiles_m = (p.m + C::BM - 1) / C::BM;
+  hipLaunchKernelGGL((gemm_f32_glds_kernel<C, STAGES>), dim3(p.tiles_m * p.tiles_n), dim3(C::NT), 0, s, p);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
+// Default: LDS-DMA kernel, 128 x 64 tiles (64 x 32 per wave), two stages
+// (48 KB LDS -> three blocks per CU) -- measured best on TDNN-S with three
+// nnet streams (tools/gemm_variants.sh: 115.5 TF vs 110.5 for the register-
+// staged 64 x 128 pipeline).  Layers it cannot take (the first layer's
+// gather, N-major MatMat operands) fall back to pipe2 64 x 128.
+// CATEARS_GEMM_VARIANT overrides for tuning.
+constexpr int kDefaultVariant = 29;
 
 int variant() {
   static int v = [] {
@@ -688,6 +887,38 @@ int launch_gemm_f32(hipStream_t s, const GemmArgs &a) {
       return deep ? launch_pipe2<V1>(s, p, a_fast, a.b_nmajor, rm) : launch_pipe2<V0>(s, p, a_fast, a.b_nmajor, rm);
     case 16:
       return deep ? launch_pipe2<V4>(s, p, a_fast, a.b_nmajor, rm) : launch_pipe2<V2>(s, p, a_fast, a.b_nmajor, rm);
+    case 20:
+      return launch_glds<V3>(s, p, a_fast, a.b_nmajor, rm);
+    case 21:
+      return launch_glds<V0>(s, p, a_fast, a.b_nmajor, rm);
+    case 22:
+      return launch_glds<V2>(s, p, a_fast, a.b_nmajor, rm);
+    case 23:
+      return launch_glds<W0>(s, p, a_fast, a.b_nmajor, rm);
+    case 24:
+      return launch_glds<W1>(s, p, a_fast, a.b_nmajor, rm);
+    case 25:
+      return launch_glds<V3, 2>(s, p, a_fast, a.b_nmajor, rm);
+    case 26:
+      return deep ? launch_glds<W2, 2>(s, p, a_fast, a.b_nmajor, rm) : launch_glds<V3>(s, p, a_fast, a.b_nmajor, rm);
+    case 27:
+      return deep ? launch_glds<W3, 2>(s, p, a_fast, a.b_nmajor, rm) : launch_glds<W0>(s, p, a_fast, a.b_nmajor, rm);
+    case 28:
+      return launch_glds<W0, 2>(s, p, a_fast, a.b_nmajor, rm);
+    case 29:
+      return launch_glds<V2, 2>(s, p, a_fast, a.b_nmajor, rm);
+    case 30:
+      return launch_glds<V8, 2>(s, p, a_fast, a.b_nmajor, rm);
+    case 31:
+      return launch_glds<W4, 2>(s, p, a_fast, a.b_nmajor, rm);
+    case 32:
+      return launch_glds<W5, 2>(s, p, a_fast, a.b_nmajor, rm);
+    case 33:
+      return launch_glds<W6, 2>(s, p, a_fast, a.b_nmajor, rm);
+    case 34:
+      return launch_glds<V0, 2>(s, p, a_fast, a.b_nmajor, rm);
+    case 35:
+      return deep ? launch_glds<V1, 2>(s, p, a_fast, a.b_nmajor, rm) : launch_glds<V0, 2>(s, p, a_fast, a.b_nmajor, rm);
     default:
       return launch_cfg<V0>(s, p, a_fast, a.b_nmajor, rm);
   }

@@ -9,8 +9,14 @@
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
+// MODE 4: as MODE 0 but the register operands are random data (MFMA power --
+// and therefore clock -- depends on operand bits).  Block 0 records its
+// s_memtime span so the effective shader clock can be derived.
+__device__ unsigned long long g_cycles;
+
 template <int MODE>
 __global__ __launch_bounds__(256) void probe(const float *__restrict__ g, float *out, int ktiles) {
+  unsigned long long t0 = __builtin_amdgcn_s_memtime();
   __shared__ __attribute__((aligned(16))) float smem[2 * 256 * 36];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
   const int wm = wave >> 1, wn = wave & 1;
@@ -20,9 +26,15 @@ __global__ __launch_bounds__(256) void probe(const float *__restrict__ g, float 
   f32x4 st[8];
   f32x4 fa[2], fb[2];
   fa[0] = fa[1] = fb[0] = fb[1] = (f32x4){1.0f, 2.0f, 3.0f, 4.0f};
+  if (MODE == 4) {
+    fa[0] = *reinterpret_cast<const f32x4 *>(g + (tid * 16 + blockIdx.x * 4096) % (65536 * 32));
+    fa[1] = *reinterpret_cast<const f32x4 *>(g + (tid * 16 + 4 + blockIdx.x * 4096) % (65536 * 32));
+    fb[0] = *reinterpret_cast<const f32x4 *>(g + (tid * 16 + 8 + blockIdx.x * 4096) % (65536 * 32));
+    fb[1] = *reinterpret_cast<const f32x4 *>(g + (tid * 16 + 12 + blockIdx.x * 4096) % (65536 * 32));
+  }
   for (int kt = 0; kt < ktiles; ++kt) {
     const float *As = smem + (kt & 1) * 256 * 36, *Bs = As + 128 * 36;
-    if (MODE >= 3) {
+    if (MODE == 3) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int idx = tid + 256 * i;
@@ -31,7 +43,7 @@ __global__ __launch_bounds__(256) void probe(const float *__restrict__ g, float 
     }
 #pragma unroll
     for (int gg = 0; gg < 4; ++gg) {
-      if (MODE >= 1) {
+      if (MODE >= 1 && MODE <= 3) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) fa[i] = *reinterpret_cast<const f32x4 *>(As + (wm * 64 + i * 32 + r) * 36 + gg * 8 + 4 * h);
 #pragma unroll
@@ -44,7 +56,7 @@ __global__ __launch_bounds__(256) void probe(const float *__restrict__ g, float 
 #pragma unroll
           for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
     }
-    if (MODE >= 3) {
+    if (MODE == 3) {
       float *An = smem + ((kt & 1) ^ 1) * 256 * 36;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
@@ -52,7 +64,7 @@ __global__ __launch_bounds__(256) void probe(const float *__restrict__ g, float 
         *reinterpret_cast<f32x4 *>(An + (idx >> 3) * 36 + 4 * (idx & 7)) = st[i];
       }
     }
-    if (MODE >= 2) __syncthreads();
+    if (MODE >= 2 && MODE <= 3) __syncthreads();
   }
   float s = 0;
 #pragma unroll
@@ -62,6 +74,7 @@ __global__ __launch_bounds__(256) void probe(const float *__restrict__ g, float 
 #pragma unroll
       for (int e = 0; e < 16; ++e) s += acc[i][j][e];
   out[blockIdx.x * 256 + tid] = s;
+  if (blockIdx.x == 0 && tid == 0) g_cycles = __builtin_amdgcn_s_memtime() - t0;
 }
 
 template <int MODE>
@@ -80,7 +93,10 @@ void run(const float *g, float *o, int blocks) {
   hipEventElapsedTime(&ms, a, b);
   ms /= iters;
   const double flops = (double)blocks * 4 * kt * 64 * 2.0 * 32 * 32 * 2;
-  printf("mode %d blocks %d: %.1f us  %.1f TFLOP/s\n", MODE, blocks, ms * 1e3, flops / (ms * 1e-3) / 1e12);
+  unsigned long long cyc = 0;
+  hipMemcpyFromSymbol(&cyc, HIP_SYMBOL(g_cycles), sizeof(cyc));
+  printf("mode %d blocks %d: %.1f us  %.1f TFLOP/s  block0 %.0f cycles (%.0f MHz if block0 spans the launch)\n", MODE,
+         blocks, ms * 1e3, flops / (ms * 1e-3) / 1e12, (double)cyc, cyc / (ms * 1e3));
 }
 
 int main() {
@@ -102,6 +118,7 @@ int main() {
     run<1>(g, o, blocks);
     run<2>(g, o, blocks);
     run<3>(g, o, blocks);
+    run<4>(g, o, blocks);
   }
   }
   return 0;
