@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the HIP-event kernel timing")
     ap.add_argument("--serial", action="store_true", help="one stream: no front/back stage overlap")
+    ap.add_argument("--workload", choices=["c3", "c2"], default="c3",
+                    help="c3: full pipeline (the headline metric); c2: batched fbank only, "
+                         "1000 x 10 s utterances per step")
     ap.add_argument("--back-streams", type=int, default=3,
                     help="nnet streams; consecutive batches alternate between them so one batch's "
                          "wave-quantisation tail overlaps the next batch's layers")
@@ -108,12 +111,13 @@ def gemm_algorithmic_bytes(rows, layers=((3072, 1024),) * 4 + ((1024, 1024), (10
     return sum(4 * (rows * k + k * n + rows * n) for k, n in layers) / len(layers)
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, workload="c3"):
     """Per-launch HBM bytes of `kernel` from the newest committed PMC summary
     (tools/pmc_traffic.py over rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
-    of this same bench); None if there is none."""
+    of this same bench and workload); None if there is none."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    pattern = "r*_pmc_traffic.json" if workload == "c3" else f"r*_{workload}_pmc_traffic.json"
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
     if not files:
         return None, None
     data = json.load(open(files[-1]))
@@ -123,8 +127,122 @@ def pmc_traffic(kernel):
     return None, None
 
 
+def cpu_fbank_baseline(n_utts, seconds, threads, min_wall):
+    """Oracle fbank ('port') on the host cores, one utterance per worker."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from catears_amd import synth
+    from oracle import pyoracle
+    n = int(16000 * seconds)
+    waves = [synth.pcm(700000 + i, n) for i in range(n_utts)]
+
+    def one(w):
+        return pyoracle.Fbank().compute(w).shape[0]
+
+    one(waves[0][:16000])
+    frames, passes = 0, 0
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        while True:
+            frames += sum(ex.map(one, waves))
+            passes += 1
+            if time.perf_counter() - t0 >= min_wall or passes >= 500:
+                break
+    dt = time.perf_counter() - t0
+    return frames / dt, frames, dt, passes
+
+
+def main_c2(args):
+    """BASELINE.json config C2: batched fbank (window + SRFFT + mel + log)
+    over 1000 x 10 s synthetic utterances resident in HBM, one launch per
+    step.  Roofline: HBM, algorithmic bytes = 4 B x samples (PCM read once)
+    + 160 B x frames (features written)."""
+    import torch
+    import torch.distributed as dist
+
+    from catears_amd import gpu, synth
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    n_utt, n_samp = 1000, int(16000 * args.seconds)
+    stream = torch.cuda.current_stream()
+    ctx = gpu.Context(local, stream)
+    plan = gpu.Plan(ctx, [n_samp] * n_utt)
+    pcm = torch.empty((n_utt, n_samp), dtype=torch.float32, device="cuda")
+    for u in range(n_utt):
+        pcm[u].copy_(torch.from_numpy(synth.pcm(rank * 100003 + u, n_samp)))
+    pcm = pcm.reshape(-1)
+    feats = torch.empty((plan.total_frames, 40), dtype=torch.float32, device="cuda")
+    for _ in range(args.warmup):
+        gpu.fbank(ctx, plan, pcm, feats)
+    torch.cuda.synchronize()
+    if not args.no_profile:
+        gpu.profile_anchor(local, stream)
+        ctx.profile(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        gpu.fbank(ctx, plan, pcm, feats)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    checksum = float(feats.double().sum().item())
+    iv = []
+    if not args.no_profile:
+        iv = ctx.profile_intervals(ctx.PROF_FBANK)
+        ctx.profile(False)
+    value = plan.total_frames * args.steps * world / elapsed
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+    roofline = None
+    bytes_per_launch = 4 * n_utt * n_samp + 4 * 40 * plan.total_frames
+    if iv:
+        avg_ms = sum(b - a for a, b in iv) / len(iv)
+        achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+        traffic, src = pmc_traffic("fbank_kernel", "c2")
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
+                    "kernel": "fbank_kernel", "launches": len(iv), "avg_launch_ms": round(avg_ms, 4),
+                    "algorithmic_bytes_per_launch": bytes_per_launch,
+                    "valu_flops_per_frame": 14000}
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        threads = min(16, os.cpu_count() or 1)
+        v, fr, dt, passes = cpu_fbank_baseline(64, args.seconds, threads, args.cpu_seconds)
+        cpu = {"value": round(v, 1), "unit": "frames/s", "cores": threads, "kind": "port",
+               "sample": f"{passes} passes over 64 x {args.seconds:g} s utterances ({fr} frames, {dt:.1f} s wall, "
+                         f"{threads} worker threads): oracle fbank (C restatement of src/fbank.cc + srfft.cc)"}
+    line = {
+        "metric": "fbank frames/sec (window+SRFFT+mel+log, 25ms/10ms, 40 bins), 16kHz",
+        "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (seeded 16 kHz PCM at raw int16 scale)",
+        "config": {"workload": f"C2 batched fbank only, {n_utt} x {args.seconds:g} s utterances per step per GPU",
+                   "frames_per_step_per_gpu": plan.total_frames, "parallelism": f"utterance shard x{world}"},
+        "roofline": roofline, "cpu_baseline": cpu, "checksum": checksum,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.workload == "c2":
+        return main_c2(args)
     import torch
     import torch.distributed as dist
 

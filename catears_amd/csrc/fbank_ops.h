@@ -27,6 +27,13 @@ CE_HD float preemph(float cur, float prev) {
   return (float)((double)cur - p);
 }
 
+// LDS placement of complex point i in the re / im arrays: a bijective XOR
+// swizzle (i ^ ((i >> 2) & 63)) that spreads the split-radix generations'
+// strided lane accesses and the bit-reversed post-pass reads over the 64 LDS
+// banks (simulated conflict passes 266 -> 146 per frame; 114 is the floor).
+// Pure placement: values and arithmetic are unchanged.
+CE_HD int sw(int i) { return i ^ ((i >> 2) & 63); }
+
 // One lane op of the split-radix generation schedule (src/srfft.cc:124-265).
 // op = kind(2) | lg(4) | n(8) | base(8); see tables.cc build_fft_schedule.
 CE_HD void fft_lane_op(uint32_t op, float *re, float *im, const float *twiddle,
@@ -36,13 +43,14 @@ CE_HD void fft_lane_op(uint32_t op, float *re, float *im, const float *twiddle,
   const int lg = (int)((op >> 2) & 15u), n = (int)((op >> 6) & 255u), base = (int)(op >> 14);
   float t1, t2;
   if (kind == 3u) {  // length-2 node (srfft.cc:206-216)
-    float *r = re + base, *i = im + base;
-    t1 = r[0] + r[1]; r[1] = r[0] - r[1]; r[0] = t1;
-    t1 = i[0] + i[1]; i[1] = i[0] - i[1]; i[0] = t1;
+    const int s0 = sw(base), s1 = sw(base + 1);
+    t1 = re[s0] + re[s1]; re[s1] = re[s0] - re[s1]; re[s0] = t1;
+    t1 = im[s0] + im[s1]; im[s1] = im[s0] - im[s1]; im[s0] = t1;
     return;
   }
   if (kind == 2u) {  // length-4 node (srfft.cc:163-205)
-    float *r = re + base, *i = im + base;
+    const int s0 = sw(base), s1 = sw(base + 1), s2 = sw(base + 2), s3 = sw(base + 3);
+    float r[4] = {re[s0], re[s1], re[s2], re[s3]}, i[4] = {im[s0], im[s1], im[s2], im[s3]};
     t1 = r[0] + r[2]; r[2] = r[0] - r[2]; r[0] = t1;
     t1 = i[0] + i[2]; i[2] = i[0] - i[2]; i[0] = t1;
     t1 = r[1] + r[3]; r[3] = r[1] - r[3]; r[1] = t1;
@@ -55,11 +63,13 @@ CE_HD void fft_lane_op(uint32_t op, float *re, float *im, const float *twiddle,
     r[3] = r[2] - i[3];
     r[2] = t1;
     i[3] = t2;
+    re[s0] = r[0]; re[s1] = r[1]; re[s2] = r[2]; re[s3] = r[3];
+    im[s0] = i[0]; im[s1] = i[1]; im[s2] = i[2]; im[s3] = i[3];
     return;
   }
   // general node of length m = 2^lg: this lane owns n, n+q, n+h, n+h+q
   const int q = 1 << (lg - 2), h = 2 * q, e = q / 2;
-  const int p0 = base + n, p1 = p0 + q, p2 = p0 + h, p3 = p2 + q;
+  const int p0 = sw(base + n), p1 = sw(base + n + q), p2 = sw(base + n + h), p3 = sw(base + n + h + q);
   float ar = re[p0], ai = im[p0], br = re[p1], bi = im[p1];
   float cr = re[p2], ci = im[p2], dr = re[p3], di = im[p3];
   // step 1: butterflies (n, n+h) and (n+q, n+q+h)
@@ -109,11 +119,11 @@ CE_HD int bitrev8(int k) {
 // with the power spectrum (src/fbank.cc:193-211).  re/im hold the complex FFT
 // before its bit-reversal permutation, so B_k is read at bitrev(k).  Writes
 // power[k] and power[256-k].
-CE_HD void post_power(int k, const float *re, const float *im, const float *kn, float *power) {
+// a, b: LDS slots of B_k and B_{256-k}, i.e. sw(bitrev8(k)), sw(bitrev8(256-k)).
+CE_HD void post_power_ab(int k, int a, int b, const float *re, const float *im, float kr, float ki,
+                         float *power) {
   const int kk = 256 - k;
-  const int a = bitrev8(k), b = bitrev8(kk & 255);
   const float xr = re[a], xi = im[a], yr = re[b], yi = im[b];
-  const float kr = kn[2 * k], ki = kn[2 * k + 1];
   // 0.5 * (float sum) in double then back to float == exact halving
   const float c_re = (float)(0.5 * (double)(xr + yr));
   const float c_im = (float)(0.5 * (double)(xi - yi));
@@ -131,9 +141,13 @@ CE_HD void post_power(int k, const float *re, const float *im, const float *kn, 
   }
 }
 
+CE_HD void post_power(int k, const float *re, const float *im, const float *kn, float *power) {
+  post_power_ab(k, sw(bitrev8(k)), sw(bitrev8((256 - k) & 255)), re, im, kn[2 * k], kn[2 * k + 1], power);
+}
+
 // DC / Nyquist bins (src/srfft.cc:446-451 then fbank.cc:203-204).
 CE_HD void edge_power(const float *re, const float *im, float *power) {
-  const float z = re[0] + im[0], nyq = re[0] - im[0];
+  const float z = re[sw(0)] + im[sw(0)], nyq = re[sw(0)] - im[sw(0)];
   power[0] = z * z;
   power[256] = nyq * nyq;
 }

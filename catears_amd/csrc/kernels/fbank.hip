@@ -30,7 +30,12 @@
 namespace catears {
 namespace {
 
-constexpr int kFramesPerBlock = 4;
+constexpr int kFramesPerBlock = 4;  // one wave per frame, 4 waves per block
+#ifndef FBANK_GENS
+#define FBANK_GENS kFftGens  // (timing experiments only may lower it)
+#endif
+constexpr int kBlocksPerCU = 6;     // residency of fbank_kernel (26 KB LDS, 78 VGPRs)
+constexpr int kMaxBlocks = 256 * kBlocksPerCU;
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -50,6 +55,20 @@ struct WaveSmem {
   float im[kHalf];
 };
 
+// Tables staged once per block in LDS (indexed by op / band at run time).
+struct BlockTables {
+  float twiddle[6 * 64 * 5];
+  float mel_w[512];
+  uint32_t ops[kFftGens * 64];
+  int twiddle_base[9];
+};
+
+// Persistent blocks: each block stages the frame-independent tables once --
+// into LDS what is indexed at run time (twiddles, generation ops, mel
+// weights), into registers what depends only on the lane (window taps,
+// post-pass twiddles and LDS slots, the lane's mel band) -- then its four
+// waves walk frames f = 4 * block + wave, f += 4 * gridDim.x.  Per frame the
+// only global traffic is the 1.6 kB PCM read and the 160 B feature write.
 __global__ __launch_bounds__(256) void fbank_kernel(const FbankTables *__restrict__ tab,
                                                     const float *__restrict__ pcm,
                                                     const int64_t *__restrict__ sample_off,
@@ -58,71 +77,92 @@ __global__ __launch_bounds__(256) void fbank_kernel(const FbankTables *__restric
                                                     int64_t total_frames, float *__restrict__ feats,
                                                     float *__restrict__ mel_out) {
   __shared__ WaveSmem smem[kFramesPerBlock];
+  __shared__ BlockTables bt;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t f = (int64_t)blockIdx.x * kFramesPerBlock + wave;
-  if (f >= total_frames) return;  // whole wave leaves; no block barrier below
+  for (int i = threadIdx.x; i < 6 * 64 * 5; i += 256) bt.twiddle[i] = tab->twiddle[i];
+  for (int i = threadIdx.x; i < 512; i += 256) bt.mel_w[i] = tab->mel_w[i];
+  for (int i = threadIdx.x; i < kFftGens * 64; i += 256) bt.ops[i] = tab->fft_ops[i];
+  if (threadIdx.x < 9) bt.twiddle_base[threadIdx.x] = tab->twiddle_base[threadIdx.x];
+  float win[7];
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    const int i = lane + 64 * j;
+    win[j] = i < kWinLen ? tab->window[i] : 0.0f;
+  }
+  const int k0 = lane + 1, k1 = lane + 65;
+  const float kn0r = tab->kn[2 * k0], kn0i = tab->kn[2 * k0 + 1];
+  const float kn1r = tab->kn[2 * k1], kn1i = tab->kn[2 * k1 + 1];
+  const int a0 = fb::sw(fb::bitrev8(k0)), b0 = fb::sw(fb::bitrev8(256 - k0));
+  const int a1 = fb::sw(fb::bitrev8(k1)), b1 = fb::sw(fb::bitrev8((256 - k1) & 255));
+  const int band = lane < kMel ? lane : 0;
+  const int mel_off = tab->mel_off[band], mel_len = lane < kMel ? tab->mel_len[band] : 0;
+  const int mel_wbase = tab->mel_wbase[band];
+  __syncthreads();
+
   WaveSmem &S = smem[wave];
+  const int64_t stride = (int64_t)gridDim.x * kFramesPerBlock;
+  for (int64_t f = (int64_t)blockIdx.x * kFramesPerBlock + wave; f < total_frames; f += stride) {
+    int u = block_utt[f / kFramesPerBlock];
+    while (f >= frame_off[u + 1]) ++u;
+    const float *src = pcm + sample_off[u] + (f - frame_off[u]) * kShift;
 
-  int u = block_utt[blockIdx.x];
-  while (f >= frame_off[u + 1]) ++u;
-  const float *src = pcm + sample_off[u] + (f - frame_off[u]) * kShift;
-
-  // 1. samples + DC offset
-  float v[7];
-  float part = 0.0f;
+    // 1. samples + DC offset (sum exact for integer-valued PCM: any order)
+    float v[7];
+    float part = 0.0f;
 #pragma unroll
-  for (int j = 0; j < 7; ++j) {
-    const int i = lane + 64 * j;
-    v[j] = i < kWinLen ? src[i] : 0.0f;
-    part += v[j];
-  }
-  const float mean = wave_sum(part) / (float)kWinLen;
-#pragma unroll
-  for (int j = 0; j < 7; ++j) {
-    const int i = lane + 64 * j;
-    if (i < kWinLen) S.x[i] = v[j] - mean;
-  }
-  wave_sync();
-
-  // 2. pre-emphasis, window, pack even/odd samples as re/im, zero pad
-#pragma unroll
-  for (int j = 0; j < 7; ++j) {
-    const int i = lane + 64 * j;
-    if (i < kWinLen) {
-      const float cur = S.x[i];
-      const float prev = i > 0 ? S.x[i - 1] : cur;
-      const float y = fb::preemph(cur, prev) * tab->window[i];
-      if (i & 1)
-        S.im[i >> 1] = y;
-      else
-        S.re[i >> 1] = y;
+    for (int j = 0; j < 7; ++j) {
+      const int i = lane + 64 * j;
+      v[j] = i < kWinLen ? src[i] : 0.0f;
+      part += v[j];
     }
-  }
-  if (lane < kHalf - kWinLen / 2) {
-    S.re[kWinLen / 2 + lane] = 0.0f;
-    S.im[kWinLen / 2 + lane] = 0.0f;
-  }
-  wave_sync();
-
-  // 3. split-radix generations
-#pragma unroll 1
-  for (int g = 0; g < kFftGens; ++g) {
-    fb::fft_lane_op(tab->fft_ops[g * 64 + lane], S.re, S.im, tab->twiddle, tab->twiddle_base);
+    const float mean = wave_sum(part) / (float)kWinLen;
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      const int i = lane + 64 * j;
+      if (i < kWinLen) S.x[i] = v[j] - mean;
+    }
     wave_sync();
-  }
 
-  // 4. real-FFT post-pass + power spectrum into S.x[0..256]
-  fb::post_power(lane + 1, S.re, S.im, tab->kn, S.x);
-  fb::post_power(lane + 65, S.re, S.im, tab->kn, S.x);
-  if (lane == 0) fb::edge_power(S.re, S.im, S.x);
-  wave_sync();
+    // 2. pre-emphasis, window, pack even/odd samples as re/im, zero pad
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      const int i = lane + 64 * j;
+      if (i < kWinLen) {
+        const float cur = S.x[i];
+        const float prev = i > 0 ? S.x[i - 1] : cur;
+        const float y = fb::preemph(cur, prev) * win[j];
+        if (i & 1)
+          S.im[fb::sw(i >> 1)] = y;
+        else
+          S.re[fb::sw(i >> 1)] = y;
+      }
+    }
+    if (lane < kHalf - kWinLen / 2) {
+      S.re[fb::sw(kWinLen / 2 + lane)] = 0.0f;
+      S.im[fb::sw(kWinLen / 2 + lane)] = 0.0f;
+    }
+    wave_sync();
 
-  // 5. mel energies, floor, log
-  if (lane < kMel) {
-    const float e = fb::mel_dot(tab->mel_w + tab->mel_wbase[lane], S.x + tab->mel_off[lane],
-                                tab->mel_len[lane]);
-    if (mel_out) mel_out[f * kMel + lane] = e;
-    feats[f * kMel + lane] = logf(e < FLT_EPSILON ? FLT_EPSILON : e);
+    // 3. split-radix generations
+#pragma unroll 1
+    for (int g = 0; g < FBANK_GENS; ++g) {
+      fb::fft_lane_op(bt.ops[g * 64 + lane], S.re, S.im, bt.twiddle, bt.twiddle_base);
+      wave_sync();
+    }
+
+    // 4. real-FFT post-pass + power spectrum into S.x[0..256]
+    fb::post_power_ab(k0, a0, b0, S.re, S.im, kn0r, kn0i, S.x);
+    fb::post_power_ab(k1, a1, b1, S.re, S.im, kn1r, kn1i, S.x);
+    if (lane == 0) fb::edge_power(S.re, S.im, S.x);
+    wave_sync();
+
+    // 5. mel energies, floor, log
+    if (lane < kMel) {
+      const float e = fb::mel_dot(bt.mel_w + mel_wbase, S.x + mel_off, mel_len);
+      if (mel_out) mel_out[f * kMel + lane] = e;
+      feats[f * kMel + lane] = logf(e < FLT_EPSILON ? FLT_EPSILON : e);
+    }
+    wave_sync();  // S.x is rewritten by the next frame
   }
 }
 
@@ -132,7 +172,8 @@ int launch_fbank(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, 
                  float *feats, float *mel) {
   if (p->total_frames == 0) return CE_GPU_OK;
   const int64_t blocks = (p->total_frames + kFramesPerBlock - 1) / kFramesPerBlock;
-  hipLaunchKernelGGL(fbank_kernel, dim3((unsigned)blocks), dim3(256), 0, s, d_tab, pcm,
+  const unsigned grid = (unsigned)(blocks < kMaxBlocks ? blocks : kMaxBlocks);
+  hipLaunchKernelGGL(fbank_kernel, dim3(grid), dim3(256), 0, s, d_tab, pcm,
                      p->d_sample_off.as<int64_t>(), p->d_frame_off.as<int64_t>(),
                      p->d_block_utt.as<int>(), p->total_frames, feats, mel);
   CE_HIP(hipGetLastError());

@@ -11,7 +11,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libcatears_hip.so")
+# CATEARS_HIP_LIB: development override (e.g. an instrumented build)
+LIB_PATH = os.environ.get("CATEARS_HIP_LIB") or os.path.join(HERE, "lib", "libcatears_hip.so")
 
 CE_GPU_OK = 0
 ERRORS = {-2: "EINVAL", -3: "EHIP", -4: "EIO", -5: "ECORRUPT", -6: "ENOTSUP", -7: "ENOMEM"}

@@ -44,9 +44,9 @@ extern "C" int emu_fbank(const float *wave, long n, float *mel, float *feats) {
     for (int i = 0; i < kWinLen; ++i) x[i] = src[i] - mean;
     for (int i = 0; i < kWinLen; ++i) {
       float y = fb::preemph(x[i], i > 0 ? x[i - 1] : x[i]) * tab.window[i];
-      if (i & 1) im[i >> 1] = y; else re[i >> 1] = y;
+      if (i & 1) im[fb::sw(i >> 1)] = y; else re[fb::sw(i >> 1)] = y;
     }
-    for (int i = kWinLen / 2; i < kHalf; ++i) re[i] = im[i] = 0.0f;
+    for (int i = kWinLen / 2; i < kHalf; ++i) re[fb::sw(i)] = im[fb::sw(i)] = 0.0f;
     for (int g = 0; g < kFftGens; ++g)
       for (int l = 0; l < 64; ++l) fb::fft_lane_op(tab.fft_ops[g * 64 + l], re, im, tab.twiddle, tab.twiddle_base);
     for (int l = 0; l < 64; ++l) {
