@@ -31,6 +31,7 @@ FLOPS_PER_FRAME = 2 * (200 * 1024 + 4 * 3072 * 1024 + 1024 * 1024 + 1024 * 3456)
 # FLOPs per output frame of the GEMMs timed as CE_GPU_PROF_GEMM (all but layer 1)
 FLOPS_PER_FRAME_FAST = FLOPS_PER_FRAME - 2 * 200 * 1024
 MFMA_F32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: dense fp32 MFMA (= vector) peak
+MFMA_I8_PEAK_TOPS = 5000.0       # MI355X_MICROARCH.md: int8 MFMA = 2x the ~2.5 PF dense bf16 rate
 HBM_PEAK_GBS = 8000.0
 METRIC = "acoustic frames/sec (fbank->nnet posteriors), 16kHz, 1/2/4/8 GPU"
 
@@ -40,7 +41,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--utts-per-step", type=int, default=4)
+    ap.add_argument("--utts-per-step", type=int, default=None, help="default 4 (c3), 8 (c5)")
     ap.add_argument("--pool", type=int, default=32, help="distinct utterances resident per rank")
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--model", default="tdnn-s")
@@ -51,9 +52,13 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the HIP-event kernel timing")
     ap.add_argument("--serial", action="store_true", help="one stream: no front/back stage overlap")
-    ap.add_argument("--workload", choices=["c3", "c2"], default="c3",
-                    help="c3: full pipeline (the headline metric); c2: batched fbank only, "
-                         "1000 x 10 s utterances per step")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL) for real runs; gloo only to rehearse N ranks on one GPU "
+                         "together with CATEARS_BENCH_DEVICE")
+    ap.add_argument("--workload", choices=["c3", "c2", "c5"], default="c3",
+                    help="c3: full pipeline fp32 (the headline metric); c2: batched fbank only, "
+                         "1000 x 10 s utterances per step; c5: full pipeline with the int8 nnet path, "
+                         "frame batch 8192")
     ap.add_argument("--back-streams", type=int, default=3,
                     help="nnet streams; consecutive batches alternate between them so one batch's "
                          "wave-quantisation tail overlaps the next batch's layers")
@@ -127,6 +132,22 @@ def pmc_traffic(kernel, workload="c3"):
     return None, None
 
 
+def device_for_rank():
+    """LOCAL_RANK's GPU; CATEARS_BENCH_DEVICE pins every rank to one device
+    (rehearsing N ranks on a one-GPU box with --dist-backend gloo)."""
+    pinned = os.environ.get("CATEARS_BENCH_DEVICE")
+    return int(pinned) if pinned is not None else int(os.environ.get("LOCAL_RANK", 0))
+
+
+def init_dist(args, local):
+    import torch
+    import torch.distributed as dist
+    if args.dist_backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group(args.dist_backend)
+
+
 def cpu_fbank_baseline(n_utts, seconds, threads, min_wall):
     """Oracle fbank ('port') on the host cores, one utterance per worker."""
     from concurrent.futures import ThreadPoolExecutor
@@ -163,10 +184,10 @@ def main_c2(args):
     from catears_amd import gpu, synth
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
+    local = device_for_rank()
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        init_dist(args, local)
     n_utt, n_samp = 1000, int(16000 * args.seconds)
     stream = torch.cuda.current_stream()
     ctx = gpu.Context(local, stream)
@@ -251,16 +272,16 @@ def main():
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
+    local = device_for_rank()
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        init_dist(args, local)
 
     # synthetic TDNN-S model, written once per node
     mdir = os.path.join(tempfile.gettempdir(), f"catears_bench_{os.getuid()}")
-    if local == 0:
+    if int(os.environ.get("LOCAL_RANK", 0)) == 0:
         synth.write_model(mdir, args.model)
     if world > 1:
         dist.barrier()
@@ -277,10 +298,14 @@ def main():
     ctxs = [gpu.Context(local, b) for b in backs]
     ctx = ctxs[0]
     ctx_f = gpu.Context(local, front) if not args.serial else ctx
+    int8 = args.workload == "c5"
     model = gpu.Model(ctx, conf)
+    if int8:
+        model.quantize(ctx)
     n_samp = int(16000 * args.seconds)
-    U = args.utts_per_step
-    plan = gpu.Plan(ctx, [n_samp] * U, model, max_rows=4096)
+    U = args.utts_per_step or (8 if int8 else 4)
+    max_rows = 8192 if int8 else 4096
+    plan = gpu.Plan(ctx, [n_samp] * U, model, max_rows=max_rows)
     frames_per_step = plan.total_frames
     assert plan.n_chunks == 1, "a step must be one frame batch"
 
@@ -371,7 +396,7 @@ def main():
             c.profile(False)
         for name, cs, cls in (("gemm", ctxs, ctx.PROF_GEMM), ("gemm_gather", ctxs, ctx.PROF_GEMM_GATHER),
                               ("fbank", [ctx_f], ctx.PROF_FBANK), ("cmvn", [ctx_f], ctx.PROF_CMVN),
-                              ("finalize", ctxs, ctx.PROF_FINALIZE)):
+                              ("finalize", ctxs, ctx.PROF_FINALIZE), ("quantize", ctxs, ctx.PROF_QUANT)):
             iv = []
             for c in cs:
                 iv += c.profile_intervals(cls)
@@ -390,7 +415,18 @@ def main():
     stages = {}
     if prof:
         ms, n, busy = prof["gemm"]
-        if n:
+        if n and int8:
+            # every Linear layer is one gemm_i8_nnet launch (class GEMM)
+            ops_per_launch = frames_per_step * FLOPS_PER_FRAME / (n / args.steps)
+            achieved = ops_per_launch * n / (busy * 1e-3) / 1e12
+            traffic, src = pmc_traffic("gemm_i8_nnet_kernel", "c5")
+            roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": MFMA_I8_PEAK_TOPS,
+                        "unit": "TOP/s", "frac": round(achieved / MFMA_I8_PEAK_TOPS, 4),
+                        "traffic": traffic, "traffic_source": src,
+                        "kernel": "gemm_i8_nnet_kernel (TDNN-S layers 1-7)",
+                        "launches": n, "avg_launch_ms": round(ms / n, 4), "busy_ms": round(busy, 3),
+                        "effective_ms_per_launch": round(busy / n, 4), "ops_per_launch": ops_per_launch}
+        elif n:
             # With several nnet streams, launches of this kernel overlap each
             # other; a launch's own duration then includes time shared with
             # its neighbour.  `achieved` is therefore the algorithmic FLOPs of
@@ -417,6 +453,19 @@ def main():
             stages["fbank"]["hbm_GBs"] = round(fb_bytes / (stages["fbank"]["avg_ms"] * 1e-3) / 1e9, 1)
             stages["fbank"]["hbm_frac"] = round(stages["fbank"]["hbm_GBs"] / HBM_PEAK_GBS, 4)
 
+    accuracy = None
+    if int8:
+        # C5's question: how far do int8 posteriors move from fp32 (one batch)
+        m32 = gpu.Model(ctx, conf)
+        first = 0
+        src = pcm[first:first + U].reshape(-1)
+        a = gpu.score(ctx, m32, plan, src, gstats).double()
+        b = gpu.score(ctx, model, plan, src, gstats).double()
+        torch.cuda.synchronize()
+        accuracy = {"frames": int(a.shape[0]), "max_abs_diff": float((a - b).abs().max().item()),
+                    "mean_abs_diff": float((a - b).abs().mean().item()),
+                    "argmax_agreement": float((a.argmax(1) == b.argmax(1)).double().mean().item())}
+
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
@@ -429,9 +478,12 @@ def main():
     line = {
         "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u8 x u8 -> int32 (fp32 features, epilogues, log-softmax)" if int8 else "fp32",
         "data": "synthetic (seeded 16 kHz PCM, random-init TDNN-S in NN02 format)",
-        "config": {"workload": "C3 full pipeline fbank->CMVN->TDNN-S->loglik, frame batch <= 4096 rows "
+        "config": {"workload": ("C5 full pipeline with the int8 nnet path (Quantize + MatMat_U8U8F32 per "
+                                f"Linear), frame batch <= {max_rows} rows " if int8 else
+                                f"C3 full pipeline fbank->CMVN->TDNN-S->loglik, frame batch <= {max_rows} rows ") +
                                f"({U} x {args.seconds:g} s utterances/step/GPU)" +
                                ("" if not gather else "; C4 RCCL gather of log-likelihoods to rank 0"),
                    "frames_per_step_per_gpu": frames_per_step, "packed_rows": plan.max_chunk_rows,
@@ -439,7 +491,9 @@ def main():
                    "streams": 1 if args.serial else 1 + NB,
                    "gather": gather},
         "roofline": roofline, "cpu_baseline": cpu, "stages": stages,
-        "end_to_end_mfma_frac": round(value / world * FLOPS_PER_FRAME / 1e12 / MFMA_F32_PEAK_TFLOPS, 4),
+        "end_to_end_mfma_frac": round(value / world * FLOPS_PER_FRAME / 1e12 /
+                                      (MFMA_I8_PEAK_TOPS if int8 else MFMA_F32_PEAK_TFLOPS), 4),
+        "int8_vs_fp32": accuracy,
         "checksum": float(checksum.item()), "finite": finite,
     }
     print(json.dumps(line), flush=True)

@@ -1,6 +1,7 @@
 // capi.cc -- extern "C" entry points of libcatears_hip (include/catears_gpu.h):
 // errors, contexts, model loading (NN02 / MAT0 / VEC0 / key=value config),
 // batch planning, and the host-side sequencing of the kernels.
+#include <float.h>
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -271,7 +272,7 @@ static int read_nnet(Reader &rd, std::vector<RawLayer> *layers, int *hl, int *hr
 static int build_program(const std::vector<RawLayer> &layers, int left, int right, ce_gpu_model *m) {
   std::vector<int> pending;  // splice offsets waiting for their Linear
   bool have_pending = false, gemm_open = false;
-  int width = -1, sum_l = 0, sum_r = 0;
+  int width = -1, sum_l = 0, sum_r = 0, pend_l = 0, pend_r = 0;
   for (size_t i = 0; i < layers.size(); ++i) {
     const RawLayer &L = layers[i];
     switch (L.id) {
@@ -285,6 +286,8 @@ static int build_program(const std::vector<RawLayer> &layers, int left, int righ
           return fail(CE_GPU_ENOTSUP, "Splice must be followed by Narrow(-min(idx,0), max(idx,0))");
         pending.assign(L.idx.begin(), L.idx.end());
         have_pending = true;
+        pend_l = -lo;
+        pend_r = hi;
         gemm_open = false;
         ++i;  // the Narrow
         sum_l += -lo;
@@ -303,6 +306,8 @@ static int build_program(const std::vector<RawLayer> &layers, int left, int righ
         if ((int)L.b.size() != out)
           return fail(CE_GPU_ECORRUPT, "Corruption: Linear bias size does not match W");
         g.nseg = have_pending ? (int)pending.size() : 1;
+        g.in_left = sum_l - (have_pending ? pend_l : 0);
+        g.in_right = sum_r - (have_pending ? pend_r : 0);
         if (in % g.nseg != 0) return fail(CE_GPU_ECORRUPT, "Corruption: Linear input does not match Splice");
         g.din = in / g.nseg;
         for (int s = 0; s < g.nseg; ++s) g.off[s] = have_pending ? pending[s] : 0;
@@ -702,6 +707,7 @@ int ce_gpu_plan_create(ce_gpu_ctx *ctx, const ce_gpu_model *model, const int64_t
     p->left = L;
     p->right = R;
     std::vector<int32_t> src, dst;
+    std::vector<uint32_t> edge;
     ce_gpu_plan::Chunk cur;
     auto close = [&]() {
       if (cur.rows > 0) {
@@ -722,7 +728,10 @@ int ce_gpu_plan_create(ce_gpu_ctx *ctx, const ce_gpu_model *model, const int64_t
           room = max_rows - L - R;
         }
         const int64_t n = std::min(T - t, room);
-        for (int64_t j = 0; j < n + L + R; ++j) {
+        const int64_t seg_rows = n + L + R;
+        for (int64_t j = 0; j < seg_rows; ++j) {
+          const uint32_t dl = (uint32_t)std::min<int64_t>(j, 0xffff), dr = (uint32_t)std::min<int64_t>(seg_rows - 1 - j, 0xffff);
+          edge.push_back(dl | (dr << 16));
           int64_t fr = t - L + j;
           fr = fr < 0 ? 0 : (fr > T - 1 ? T - 1 : fr);
           src.push_back((int32_t)(p->frame_off[u] + fr));
@@ -736,6 +745,7 @@ int ce_gpu_plan_create(ce_gpu_ctx *ctx, const ce_gpu_model *model, const int64_t
     if (!src.empty()) {
       CE_TRY(p->d_row_src.upload(src.data(), src.size() * 4));
       CE_TRY(p->d_row_dst.upload(dst.data(), dst.size() * 4));
+      CE_TRY(p->d_row_edge.upload(edge.data(), edge.size() * 4));
     }
   }
   *out = p.release();
@@ -787,8 +797,8 @@ namespace catears {
 // Runs the program's steps on `rows` packed rows starting at x (row_map: the
 // first layer's packed row -> source row, or NULL for identity).  Returns the
 // last activation via *y / *ldy.
-static int run_steps(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, int ldx, int rows,
-                     const int *row_map, const float **y, int *ldy) {
+static int run_steps_f32(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, int ldx, int rows,
+                         const int *row_map, const float **y, int *ldy) {
   const size_t per = (size_t)rows * m->max_width;
   CE_TRY(ensure_workspace(ctx, 2 * per));
   float *buf[2] = {ctx->workspace.as<float>(), ctx->workspace.as<float>() + per};
@@ -833,6 +843,120 @@ static int run_steps(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, int
   *ldy = ldx;
   return CE_GPU_OK;
 }
+// The int8 program (kernels/nnet_i8.hip): per Linear layer min/max ->
+// quantize (+ row sums) -> u8 GEMM with float epilogue.
+static int run_steps_i8(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, int ldx, int rows,
+                        const int *row_map, const uint32_t *row_edge, const float **y, int *ldy) {
+  const size_t per = (size_t)rows * m->max_width;
+  CE_TRY(ensure_workspace(ctx, 2 * per));
+  float *buf[2] = {ctx->workspace.as<float>(), ctx->workspace.as<float>() + per};
+  int max_ldq = 16;
+  for (const Step &st : m->steps)
+    if (st.is_gemm) max_ldq = std::max(max_ldq, st.i8.spliced ? st.i8.kpad : st.i8.in_width);
+  const size_t q_bytes = ((size_t)rows * max_ldq + 255) / 256 * 256;
+  const size_t rs_bytes = ((size_t)rows * 4 + 255) / 256 * 256;
+  CE_TRY(ensure_scratch(ctx, q_bytes + rs_bytes + 256 + i8_params_scratch_bytes()));
+  char *base = static_cast<char *>(ctx->scratch.ptr);
+  int8_t *xq = reinterpret_cast<int8_t *>(base);
+  int32_t *rowsum = reinterpret_cast<int32_t *>(base + q_bytes);
+  void *params = base + q_bytes + rs_bytes;
+  void *part = base + q_bytes + rs_bytes + 256;
+  int cur = 0;
+  bool first = true;
+  for (const Step &st : m->steps) {
+    if (st.is_gemm) {
+      const I8Layer &L = st.i8;
+      const int *rm = first ? row_map : nullptr;
+      const int ldq = L.spliced ? L.kpad : L.in_width;
+      {
+        ProfScope prof(ctx, CE_GPU_PROF_QUANT);
+        CE_TRY(launch_i8_params(ctx->stream, x, ldx, rows, L.in_width, rm, row_edge, L.in_left, L.in_right,
+                                part, params));
+        if (L.spliced) {
+          CE_TRY(launch_i8_quantize(ctx->stream, x, ldx, rows, L.in_width, rm, st.gemm.nseg, st.gemm.off, params,
+                                    xq, ldq, rowsum));
+        } else {
+          const int zero[1] = {0};
+          CE_TRY(launch_i8_quantize(ctx->stream, x, ldx, rows, L.in_width, rm, 1, zero, params, xq, ldq, rowsum));
+        }
+      }
+      ProfScope prof(ctx, CE_GPU_PROF_GEMM);
+      CE_TRY(launch_i8_gemm(ctx->stream, L, xq, ldq, rows, rowsum, params, buf[cur], L.n));
+      x = buf[cur];
+      ldx = L.n;
+      cur ^= 1;
+      first = false;
+    } else {
+      CE_TRY(launch_rowop(ctx->stream, st.row, const_cast<float *>(x), ldx, rows));
+    }
+  }
+  *y = x;
+  *ldy = ldx;
+  return CE_GPU_OK;
+}
+
+static int run_steps(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, int ldx, int rows,
+                     const int *row_map, const uint32_t *row_edge, const float **y, int *ldy) {
+  return m->int8 ? run_steps_i8(ctx, m, x, ldx, rows, row_map, row_edge, y, ldy)
+                 : run_steps_f32(ctx, m, x, ldx, rows, row_map, y, ldy);
+}
+
+// Quantize (src/matrix.cc:329-387) of one weight matrix on the host at load
+// time: per-tensor parameters over the in x out MAT0 matrix, then the bytes
+// stored shifted (q - 128) and transposed (n x kpad, zero padded) for the
+// GEMM, with their column sums.
+static int quantize_weights(ce_gpu_ctx *ctx, Step &st) {
+  GemmLayer &g = st.gemm;
+  I8Layer &L = st.i8;
+  std::vector<float> wt((size_t)g.n * g.kpad);
+  CE_HIP(hipMemcpy(wt.data(), g.wt.ptr, wt.size() * 4, hipMemcpyDeviceToHost));
+  float mn = FLT_MAX, mx = FLT_MIN;  // FindMinMax (matrix.cc:329-345)
+  for (int j = 0; j < g.n; ++j)
+    for (int k = 0; k < g.k; ++k) {
+      const float v = wt[(size_t)j * g.kpad + k];
+      if (v > mx) mx = v;
+      if (v < mn) mn = v;
+    }
+  const double scale = (mx - mn) / 255.0;  // ComputeQuantizationParams (matrix.cc:348-362)
+  L.w_zp = (int32_t)round(-mn / scale);
+  L.w_scale = (float)scale;
+  const int ka = i8_k_align();
+  L.n = g.n;
+  L.k = g.k;
+  L.kpad = (g.k + ka - 1) / ka * ka;
+  std::vector<int8_t> q((size_t)g.n * L.kpad, 0);
+  std::vector<int32_t> colsum(g.n, 0);
+  for (int j = 0; j < g.n; ++j)
+    for (int k = 0; k < g.k; ++k) {
+      float v = wt[(size_t)j * g.kpad + k] / L.w_scale + L.w_zp;  // matrix.cc:378-386
+      v = std::max(0.0f, std::min(v, 255.0f));
+      const int b = (int)(uint8_t)roundf(v) - 128;
+      q[(size_t)j * L.kpad + k] = (int8_t)b;
+      colsum[j] += b;
+    }
+  CE_TRY(L.wq.upload(q.data(), q.size()));
+  CE_TRY(L.colsum.upload(colsum.data(), colsum.size() * 4));
+  L.in_width = g.din;
+  L.in_left = g.in_left;
+  L.in_right = g.in_right;
+  L.spliced = g.din % ka != 0;
+  if (L.spliced) {
+    L.a_din = L.kpad;
+    L.a_nseg = 1;
+    for (int i = 0; i < 8; ++i) L.a_off[i] = 0;
+  } else {
+    L.a_din = g.din;
+    L.a_nseg = g.nseg;
+    for (int i = 0; i < 8; ++i) L.a_off[i] = g.off[i];
+  }
+  L.bias = g.bias.as<float>();
+  L.bn_scale = g.bn_scale.as<float>();
+  L.bn_offset = g.bn_offset.as<float>();
+  for (int i = 0; i < 4; ++i) L.post[i] = g.post[i];
+  L.npost = g.npost;
+  (void)ctx;
+  return CE_GPU_OK;
+}
 }  // namespace catears
 
 extern "C" {
@@ -852,7 +976,8 @@ int ce_gpu_am_forward(ce_gpu_ctx *ctx, const ce_gpu_model *m, const ce_gpu_plan 
     const int *row_dst = p->d_row_dst.as<int>() + c.map_base;
     const float *y = nullptr;
     int ldy = 0;
-    CE_TRY(run_steps(ctx, m, d_feats, m->input_dim, c.rows, row_src, &y, &ldy));
+    const uint32_t *row_edge = p->d_row_edge.as<uint32_t>() + c.map_base;
+    CE_TRY(run_steps(ctx, m, d_feats, m->input_dim, c.rows, row_src, row_edge, &y, &ldy));
     ProfScope prof(ctx, CE_GPU_PROF_FINALIZE);
     CE_TRY(launch_finalize(ctx->stream, y, ldy, c.rows, m->num_pdfs, m->final_log_softmax,
                            m->log_prior.as<float>(), row_dst, d_loglik));
@@ -886,7 +1011,7 @@ int ce_gpu_nnet_propagate(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *d
   if (subtract_prior && !m->log_prior.ptr) return fail(CE_GPU_EINVAL, "model has no prior");
   const float *y = nullptr;
   int ldy = 0;
-  CE_TRY(run_steps(ctx, m, d_in, ld_in, rows, nullptr, &y, &ldy));
+  CE_TRY(run_steps(ctx, m, d_in, ld_in, rows, nullptr, nullptr, &y, &ldy));
   ProfScope prof(ctx, CE_GPU_PROF_FINALIZE);
   return launch_finalize(ctx->stream, y + (size_t)m->net_left * ldy, ldy, out_rows, m->num_pdfs,
                          m->final_log_softmax, subtract_prior ? m->log_prior.as<float>() : nullptr, nullptr,
@@ -1005,6 +1130,16 @@ int ce_gpu_rowwise(ce_gpu_ctx *ctx, int op, int rows, int dim, float *d_x, int l
   if (rows == 0 || dim == 0) return CE_GPU_OK;
   if (!d_x) return fail(CE_GPU_EINVAL, "NULL argument");
   return launch_rowop_raw(ctx->stream, op, dim, d_scale, d_offset, d_x, ld, rows);
+}
+
+int ce_gpu_model_quantize(ce_gpu_ctx *ctx, ce_gpu_model *m) {
+  if (!ctx || !m) return fail(CE_GPU_EINVAL, "NULL argument");
+  if (m->int8) return CE_GPU_OK;
+  CE_HIP(hipSetDevice(ctx->device));
+  for (Step &st : m->steps)
+    if (st.is_gemm) CE_TRY(quantize_weights(ctx, st));
+  m->int8 = true;
+  return CE_GPU_OK;
 }
 
 }  // extern "C"

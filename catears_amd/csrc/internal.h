@@ -105,9 +105,33 @@ struct GemmLayer {
   DevBuf bn_scale, bn_offset;  // n, when a BatchNorm is fused
   int post[4] = {0, 0, 0, 0};
   int npost = 0;
+  // rows of the block entering this layer's Splice that the reference chain
+  // still holds: the Narrows before it dropped in_left / in_right rows
+  int in_left = 0, in_right = 0;
 };
 
 // Same numbering as the ABI's CE_GPU_ROW_* (checked in capi.cc).
+// int8 form of one Linear layer (kernels/nnet_i8.hip), built by
+// ce_gpu_model_quantize.  The A operand is the quantized layer input: either
+// read through the splice offsets (segment width a_din a multiple of the
+// 64-byte K-tile) or, when `spliced`, written already spliced by the
+// quantize pass (a_nseg = 1, a_din = kpad).
+struct I8Layer {
+  DevBuf wq;                   // n x kpad, (u8 - 128), zero padded
+  DevBuf colsum;               // n int32: sums of the shifted weight bytes
+  int n = 0, k = 0, kpad = 0;
+  float w_scale = 0.0f;
+  int32_t w_zp = 0;
+  bool spliced = false;
+  int in_width = 0;            // width of the float layer input
+  int a_din = 0, a_nseg = 1;
+  int a_off[8] = {0};
+  int in_left = 0, in_right = 0;  // see GemmLayer
+  const float *bias = nullptr, *bn_scale = nullptr, *bn_offset = nullptr;
+  int post[4] = {0, 0, 0, 0};
+  int npost = 0;
+};
+
 enum RowOpKind : int { kRowRelu, kRowBatchNorm, kRowLogSoftmax, kRowSoftmax, kRowNormalize };
 
 struct RowOp {
@@ -120,6 +144,7 @@ struct RowOp {
 struct Step {
   bool is_gemm = true;
   GemmLayer gemm;
+  I8Layer i8;  // filled by ce_gpu_model_quantize
   RowOp row;
 };
 
@@ -162,6 +187,7 @@ struct ce_gpu_model {
   int input_dim = 0, num_pdfs = 0, num_linear = 0, max_width = 0;
   int64_t num_params = 0;
   bool final_log_softmax = false;
+  bool int8 = false;                 // Linear layers run as Quantize + u8 GEMM
   std::vector<catears::Step> steps;  // all but the final log-softmax
   catears::DevBuf log_prior;         // num_pdfs
   std::vector<int32_t> tid2pdf;
@@ -182,6 +208,7 @@ struct ce_gpu_plan {
   std::vector<Chunk> chunks;
   catears::DevBuf d_row_src;  // int32 per packed row: source feature row
   catears::DevBuf d_row_dst;  // int32 per packed row: output row or -1
+  catears::DevBuf d_row_edge; // uint32 per packed row: rows to its segment's start | end << 16
   int max_chunk_rows = 0;
   int left = 0, right = 0;
   bool has_model = false;
@@ -228,6 +255,18 @@ int launch_splice(hipStream_t s, int rows, int dim, const float *in, int ld_in, 
 int launch_quantize(hipStream_t s, const float *x, int64_t count, uint8_t *q, void *params,
                     void *scratch);
 size_t gemm_u8_scratch_bytes(int m, int n, int k);
+// int8 nnet path (kernels/nnet_i8.hip)
+// min / max over the rows the reference chain holds: row r counts when its
+// distances to its segment's edges (row_edge, or r / rows-1-r for one
+// segment) are >= in_left / in_right.
+int launch_i8_params(hipStream_t s, const float *x, int ldx, int rows, int width, const int *row_map,
+                     const uint32_t *row_edge, int in_left, int in_right, void *part, void *params);
+size_t i8_params_scratch_bytes();
+int launch_i8_quantize(hipStream_t s, const float *x, int ldx, int rows, int width, const int *row_map, int nseg,
+                       const int *offs, const void *params, int8_t *q, int ldq, int32_t *rowsum);
+int launch_i8_gemm(hipStream_t s, const I8Layer &L, const int8_t *a, int lda, int m, const int32_t *rowsum,
+                   const void *pa, float *y, int ldy);
+int i8_k_align();
 int launch_gemm_u8_ws(hipStream_t s, int m, int n, int k, const uint8_t *a, const void *pa,
                       const uint8_t *b, const void *pb, float *c_f32, int32_t *c_i32, void *ws);
 

@@ -1,0 +1,539 @@
+// nnet_i8.hip -- the int8 nnet path (BASELINE config C5): every LinearLayer
+// as Quantize + MatMat_U8U8F32 + bias (src/matrix.cc:329-420, the pieces the
+// reference ships but never wires into Nnet, src/nnet.cc:29).
+//
+// Per layer and per chunk of packed rows:
+//   1. minmax_kernel     min / max over the layer input X (rows x width; the
+//      params_kernel     first layer reads its rows through row_map): block
+//                        partials, then one block folds them, both seeded
+//                        with FLT_MAX and FLT_MIN exactly like FindMinMax
+//                        (matrix.cc:331-345: max starts at FLT_MIN), and
+//                        applies ComputeQuantizationParams (matrix.cc:348-362).
+//                        Only rows the reference chain still holds count: the
+//                        packed buffers keep full height, so the edge rows the
+//                        earlier Narrows dropped (computed from clamped
+//                        indices) are skipped by their distance to the
+//                        segment edges.
+//   2. quantize_kernel   q = roundf(clamp(x / scale + zp, 0, 255)) stored as the
+//                        signed byte q ^ 0x80 = q - 128, with the row sums of
+//                        those bytes.  Layers whose segment width is not a
+//                        multiple of the 64-byte K-tile (the 40-wide first layer)
+//                        are written already spliced (rows x K, zero padded).
+//   3. gemm_i8_nnet      v_mfma_i32_32x32x32_i8 on the shifted bytes with the
+//                        splice folded into the A loader; int32 epilogue
+//                        restores the zero points,
+//                          sum (a-zA)(b-zB) = sum a'b' + cB*rowsum(a') + cA*colsum(b') + K*cA*cB
+//                        (cA = 128 - zA), all modulo 2^32 like gemmlowp's
+//                        accumulator, then float(acc) * (sA*sB) + bias, ReLU /
+//                        BatchNorm in the reference's rounding order.
+// Quantising the block entering the Splice is the same as quantising the
+// spliced block: the tensor parameters depend only on min / max, and Splice +
+// Narrow read every held row of the block.
+#include <float.h>
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdlib.h>
+
+#include "../internal.h"
+#include "../tile_order.h"
+
+namespace catears {
+namespace {
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+
+// One wave per row (grid-stride over rows); rows outside what the reference
+// chain holds at this layer (segment edges already narrowed away) are skipped.
+// Each block leaves one (min, max) partial; params_kernel folds them.
+constexpr int kMinmaxBlocks = 512;
+
+__global__ __launch_bounds__(256) void minmax_kernel(const float *__restrict__ x, int ldx, int rows, int width,
+                                                     const int *__restrict__ row_map,
+                                                     const uint32_t *__restrict__ row_edge, int in_left,
+                                                     int in_right, float2 *__restrict__ part) {
+  float mn = FLT_MAX, mx = FLT_MIN;
+  const int lane = threadIdx.x & 63;
+  for (int r = blockIdx.x * 4 + (threadIdx.x >> 6); r < rows; r += gridDim.x * 4) {
+    const int dl = row_edge ? (int)(row_edge[r] & 0xffff) : r;
+    const int dr = row_edge ? (int)(row_edge[r] >> 16) : rows - 1 - r;
+    if (dl < in_left || dr < in_right) continue;
+    const int src = row_map ? row_map[r] : r;
+    const float *xr = x + (int64_t)src * ldx;
+    if ((width & 3) == 0 && (ldx & 3) == 0) {
+      for (int c = 4 * lane; c < width; c += 256) {
+        const float4 v = *reinterpret_cast<const float4 *>(xr + c);
+        const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          if (e[t] > mx) mx = e[t];  // matrix.cc:337-342 (NaN never wins a comparison)
+          if (e[t] < mn) mn = e[t];
+        }
+      }
+    } else {
+      for (int c = lane; c < width; c += 64) {
+        const float v = xr[c];
+        if (v > mx) mx = v;
+        if (v < mn) mn = v;
+      }
+    }
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const float omn = __shfl_xor(mn, d, 64), omx = __shfl_xor(mx, d, 64);
+    mn = omn < mn ? omn : mn;
+    mx = omx > mx ? omx : mx;
+  }
+  __shared__ float2 wv[4];
+  if (lane == 0) wv[threadIdx.x >> 6] = make_float2(mn, mx);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w) {
+      mn = wv[w].x < mn ? wv[w].x : mn;
+      mx = wv[w].y > mx ? wv[w].y : mx;
+    }
+    part[blockIdx.x] = make_float2(mn, mx);
+  }
+}
+
+struct QP {
+  float scale;
+  int32_t zp;
+};
+
+// Folds the block partials and applies ComputeQuantizationParams
+// (matrix.cc:348-362, double arithmetic) -- one block.
+__global__ __launch_bounds__(256) void params_kernel(const float2 *__restrict__ part, int nparts,
+                                                     QP *__restrict__ out) {
+  float mn = FLT_MAX, mx = FLT_MIN;
+  for (int i = threadIdx.x; i < nparts; i += 256) {
+    mn = part[i].x < mn ? part[i].x : mn;
+    mx = part[i].y > mx ? part[i].y : mx;
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const float omn = __shfl_xor(mn, d, 64), omx = __shfl_xor(mx, d, 64);
+    mn = omn < mn ? omn : mn;
+    mx = omx > mx ? omx : mx;
+  }
+  __shared__ float2 wv[4];
+  if ((threadIdx.x & 63) == 0) wv[threadIdx.x >> 6] = make_float2(mn, mx);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w) {
+      mn = wv[w].x < mn ? wv[w].x : mn;
+      mx = wv[w].y > mx ? wv[w].y : mx;
+    }
+    const double scale = (mx - mn) / 255.0;
+    QP p;
+    p.zp = (int32_t)round(-mn / scale);
+    p.scale = (float)scale;
+    *out = p;
+  }
+}
+
+// Quantize (matrix.cc:378-386) of one element -> shifted signed byte.
+__device__ __forceinline__ int qbyte(float x, float scale, float zp) {
+  float v = x / scale + zp;
+  v = (255.0f < v) ? 255.0f : v;  // std::min(v, 255.0f)
+  v = (0.0f < v) ? v : 0.0f;      // std::max(0.0f, v)
+  return (int)(uint8_t)roundf(v) - 128;
+}
+
+// One wave per output row.  Plain mode: out row r = quantized X row
+// (row_map[r] or r), width bytes, zero padded to ldq.  Spliced mode (nseg >
+// 1 or width % 64): out row r = concat over segments s of quantized
+// X[clamp(r + off[s])] (through row_map), zero padded to ldq.
+struct SpliceOffsets {
+  int off[8];
+};
+
+__global__ __launch_bounds__(256) void quantize_kernel(const float *__restrict__ x, int ldx, int rows, int width,
+                                                       const int *__restrict__ row_map, int nseg,
+                                                       SpliceOffsets so, const QP *__restrict__ params,
+                                                       int8_t *__restrict__ q, int ldq, int32_t *__restrict__ rowsum) {
+  const QP p = *params;
+  const float zp = (float)p.zp;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  int8_t *o = q + (int64_t)r * ldq;
+  int32_t s = 0;
+  const bool vec = (width & 3) == 0 && (ldx & 3) == 0;
+  for (int seg = 0; seg < nseg; ++seg) {
+    int src = r + so.off[seg];
+    src = src < 0 ? 0 : (src > rows - 1 ? rows - 1 : src);
+    if (row_map) src = row_map[src];
+    const float *xr = x + (int64_t)src * ldx;
+    int8_t *os = o + seg * width;
+    if (vec) {
+      for (int c = 4 * lane; c < width; c += 256) {
+        const float4 v = *reinterpret_cast<const float4 *>(xr + c);
+        const int b0 = qbyte(v.x, p.scale, zp), b1 = qbyte(v.y, p.scale, zp);
+        const int b2 = qbyte(v.z, p.scale, zp), b3 = qbyte(v.w, p.scale, zp);
+        s += b0 + b1 + b2 + b3;
+        const uint32_t packed = (uint32_t)(uint8_t)b0 | ((uint32_t)(uint8_t)b1 << 8) |
+                                ((uint32_t)(uint8_t)b2 << 16) | ((uint32_t)(uint8_t)b3 << 24);
+        if ((((uintptr_t)(os + c)) & 3) == 0) {
+          *reinterpret_cast<uint32_t *>(os + c) = packed;
+        } else {
+          os[c] = (int8_t)b0, os[c + 1] = (int8_t)b1, os[c + 2] = (int8_t)b2, os[c + 3] = (int8_t)b3;
+        }
+      }
+    } else {
+      for (int c = lane; c < width; c += 64) {
+        const int b = qbyte(xr[c], p.scale, zp);
+        os[c] = (int8_t)b;
+        s += b;
+      }
+    }
+  }
+  for (int c = nseg * width + lane; c < ldq; c += 64) o[c] = 0;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
+  if (lane == 0) rowsum[r] = s;
+}
+
+constexpr int IBM = 128, IBN = 128, IBK = 64, ILD = IBK + 16;  // bytes
+
+struct I8Args {
+  const int8_t *a;          // quantized layer input (rows x lda bytes)
+  int lda, m;
+  int din, nseg;            // segment width (bytes) and count; K = din * nseg
+  int off[8];
+  const int32_t *rowsum;    // per row of `a`
+  const int8_t *w;          // shifted weights, n x kpad
+  const int32_t *colsum;    // per column of w (shifted bytes)
+  int n, k, kpad;
+  const void *pa;           // device QP of the activations
+  float w_scale;
+  int32_t w_zp;
+  const float *bias, *bn_scale, *bn_offset;
+  int post[4];
+  int npost;
+  float *y;
+  int ldy;
+  int tiles_n, tiles_m, group;
+};
+
+__global__ __launch_bounds__(256, 2) void gemm_i8_nnet_kernel(I8Args p) {
+  __shared__ __attribute__((aligned(16))) int8_t As[IBM * ILD];
+  __shared__ __attribute__((aligned(16))) int8_t Bs[IBN * ILD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, r = lane & 31, h = lane >> 5;
+  const int tm = blockIdx.x / p.tiles_n, tn = blockIdx.x - tm * p.tiles_n;
+  const int m0 = tm * IBM, n0 = tn * IBN;
+
+  i32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0;
+
+  for (int k0 = 0; k0 < p.kpad; k0 += IBK) {
+    // one K-tile never straddles a segment (din % 64 == 0 or nseg == 1)
+    const int seg = k0 / p.din, col0 = k0 - seg * p.din;
+    const int shift = p.off[seg < 8 ? seg : 7];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int idx = tid + 256 * i, row = idx >> 2, c16 = idx & 3;
+      int src = m0 + row + shift;
+      src = src < 0 ? 0 : (src > p.m - 1 ? p.m - 1 : src);
+      i32x4 v = (i32x4){0, 0, 0, 0};
+      if (col0 + 16 * c16 < p.din && k0 < p.k)
+        v = *reinterpret_cast<const i32x4 *>(p.a + (int64_t)src * p.lda + col0 + 16 * c16);
+      *reinterpret_cast<i32x4 *>(As + row * ILD + 16 * c16) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int idx = tid + 256 * i, row = idx >> 2, c16 = idx & 3;
+      const int gn = min(n0 + row, p.n - 1);
+      *reinterpret_cast<i32x4 *>(Bs + row * ILD + 16 * c16) =
+          *reinterpret_cast<const i32x4 *>(p.w + (int64_t)gn * p.kpad + k0 + 16 * c16);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < IBK / 32; ++s) {
+      i32x4 af[2], bf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        af[i] = *reinterpret_cast<const i32x4 *>(As + (wm * 64 + i * 32 + r) * ILD + 32 * s + 16 * h);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        bf[j] = *reinterpret_cast<const i32x4 *>(Bs + (wn * 64 + j * 32 + r) * ILD + 32 * s + 16 * h);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  const QP pa = *static_cast<const QP *>(p.pa);
+  const uint32_t ca = (uint32_t)(128 - pa.zp), cb = (uint32_t)(128 - p.w_zp);
+  const uint32_t kterm = (uint32_t)p.k * ca * cb;
+  const float cscale = pa.scale * p.w_scale;  // matrix.cc:404-405
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int row = m0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+      if (row >= p.m) continue;
+      uint32_t rs = 0;  // row sum of the spliced row
+      for (int sg = 0; sg < p.nseg; ++sg) {
+        int src = row + p.off[sg];
+        src = src < 0 ? 0 : (src > p.m - 1 ? p.m - 1 : src);
+        rs += (uint32_t)p.rowsum[src];
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = n0 + wn * 64 + j * 32 + r;
+        if (col >= p.n) continue;
+        const uint32_t v = (uint32_t)acc[i][j][e] + cb * rs + ca * (uint32_t)p.colsum[col] + kterm;
+        float y = (float)(int32_t)v * cscale;
+        if (p.bias) y = y + p.bias[col];
+        for (int q = 0; q < p.npost; ++q) {
+          if (p.post[q] == kPostRelu) {
+            y = y < 0.0f ? 0.0f : y;
+          } else if (p.post[q] == kPostBatchNorm) {
+            y = y * p.bn_scale[col];
+            y = y + p.bn_offset[col];
+          }
+        }
+        p.y[(int64_t)row * p.ldy + col] = y;
+      }
+    }
+  }
+}
+
+
+// LDS-DMA form of the int8 GEMM (the fp32 kernel's structure, gemm_f32.hip):
+// K-tiles of 128 bytes, global_load_lds_dwordx4 into two LDS stages with the
+// XOR chunk swizzle applied on the source address, one barrier per K-tile.
+// A 32x32x32 i8 MFMA operand is one ds_read_b128 per lane (row r, bytes
+// 16h..16h+15 of its 32-byte k-step), so a tile row of 128 bytes holds the
+// four k-steps of the tile.  BM x BN block tile, 2 x 2 waves.
+template <int BM, int BN, int STAGES>
+__global__ __launch_bounds__(256, 1) void gemm_i8_glds_kernel(I8Args p) {
+  constexpr int BKB = 128;                  // bytes per K-tile row
+  constexpr int TI = BM / 2 / 32, TJ = BN / 2 / 32;
+  constexpr int RPI = 1024 / BKB;           // rows per DMA instruction (8)
+  constexpr int NGA = BM * BKB / 1024 / 4, NGB = BN * BKB / 1024 / 4;
+  constexpr int STAGE = (BM + BN) * BKB;    // bytes
+  static_assert(NGA >= 1 && NGB >= 1, "tile too small");
+  __shared__ __attribute__((aligned(1024))) int8_t smem[STAGES * STAGE];
+  auto swz = [](int row) { return (row >> 1) & 7; };
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, r = lane & 31, h = lane >> 5;
+  int tm, tn;
+  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int lrow = lane / 8, lchunk = lane & 7;
+  uint32_t boff[NGB];
+#pragma unroll
+  for (int j = 0; j < NGB; ++j) {
+    const int row = (wave * NGB + j) * RPI + lrow;
+    boff[j] = (uint32_t)(min(n0 + row, p.n - 1) * p.kpad + 16 * (lchunk ^ swz(row)));
+  }
+  uint32_t aoff[NGA];
+  int cur_seg = -1;
+  auto issue = [&](int kt) {
+    const int k0 = kt * BKB;
+    const int seg = k0 / p.din, col0 = k0 - seg * p.din;
+    if (seg != cur_seg) {
+      cur_seg = seg;
+      const int shift = p.off[seg < 8 ? seg : 7];
+#pragma unroll
+      for (int i = 0; i < NGA; ++i) {
+        const int row = (wave * NGA + i) * RPI + lrow;
+        int src = m0 + row + shift;
+        src = src < 0 ? 0 : (src > p.m - 1 ? p.m - 1 : src);
+        aoff[i] = (uint32_t)(src * p.lda + 16 * (lchunk ^ swz(row)));
+      }
+    }
+    int8_t *st = smem + (kt % STAGES) * STAGE;
+    const char *abase = reinterpret_cast<const char *>(p.a) + col0;
+    const char *bbase = reinterpret_cast<const char *>(p.w) + k0;
+#pragma unroll
+    for (int i = 0; i < NGA; ++i)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(abase + aoff[i]),
+                                       (__attribute__((address_space(3))) void *)(st + (wave * NGA + i) * 1024), 16,
+                                       0, 0);
+#pragma unroll
+    for (int j = 0; j < NGB; ++j)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(bbase + boff[j]),
+                                       (__attribute__((address_space(3))) void *)(st + BM * BKB + (wave * NGB + j) * 1024),
+                                       16, 0, 0);
+  };
+
+  i32x16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0;
+
+  const int xr = swz(r) ^ h;  // chunk 2s + h -> (2s) ^ xr
+  const int a_row = (wm * TI * 32 + r) * BKB, b_row = BM * BKB + (wn * TJ * 32 + r) * BKB;
+  const int ktiles = p.kpad / BKB;
+  // STAGES-1 tiles in flight: tile kt has landed once at most STAGES-2 newer
+  // tiles' DMAs are outstanding (counted vmcnt, raw barrier: the DMAs stay in
+  // flight across it); the stage refilled at kt is the one read at kt-1.
+  constexpr int NG = NGA + NGB;
+  for (int t = 0; t < STAGES - 1 && t < ktiles; ++t) issue(t);
+  for (int kt = 0; kt < ktiles; ++kt) {
+    const int ahead = min(ktiles - 1 - kt, STAGES - 2);  // newer tiles already issued
+    if (ahead >= 2)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NG) : "memory");
+    else if (ahead == 1)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NG) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + STAGES - 1 < ktiles) issue(kt + STAGES - 1);
+    const int8_t *st = smem + (kt % STAGES) * STAGE;
+#pragma unroll
+    for (int s = 0; s < BKB / 32; ++s) {
+      const int ch = ((2 * s) ^ xr) * 16;
+      i32x4 af[TI], bf[TJ];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) af[i] = *reinterpret_cast<const i32x4 *>(st + a_row + i * 32 * BKB + ch);
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) bf[j] = *reinterpret_cast<const i32x4 *>(st + b_row + j * 32 * BKB + ch);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  const QP pa = *static_cast<const QP *>(p.pa);
+  const uint32_t ca = (uint32_t)(128 - pa.zp), cb = (uint32_t)(128 - p.w_zp);
+  const uint32_t kterm = (uint32_t)p.k * ca * cb;
+  const float cscale = pa.scale * p.w_scale;  // matrix.cc:404-405
+#pragma unroll
+  for (int i = 0; i < TI; ++i) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int row = m0 + wm * TI * 32 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+      if (row >= p.m) continue;
+      uint32_t rs = 0;  // row sum of the spliced row
+      for (int sg = 0; sg < p.nseg; ++sg) {
+        int src = row + p.off[sg];
+        src = src < 0 ? 0 : (src > p.m - 1 ? p.m - 1 : src);
+        rs += (uint32_t)p.rowsum[src];
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int col = n0 + wn * TJ * 32 + j * 32 + r;
+        if (col >= p.n) continue;
+        const uint32_t v = (uint32_t)acc[i][j][e] + cb * rs + ca * (uint32_t)p.colsum[col] + kterm;
+        float y = (float)(int32_t)v * cscale;
+        if (p.bias) y = y + p.bias[col];
+        for (int q = 0; q < p.npost; ++q) {
+          if (p.post[q] == kPostRelu) {
+            y = y < 0.0f ? 0.0f : y;
+          } else if (p.post[q] == kPostBatchNorm) {
+            y = y * p.bn_scale[col];
+            y = y + p.bn_offset[col];
+          }
+        }
+        p.y[(int64_t)row * p.ldy + col] = y;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+// Reduces the held rows of a layer input to QP params (minmax partials in
+// `part`, kMinmaxBlocks float2).
+int launch_i8_params(hipStream_t s, const float *x, int ldx, int rows, int width, const int *row_map,
+                     const uint32_t *row_edge, int in_left, int in_right, void *part, void *params) {
+  const int blocks = std::max(1, std::min(kMinmaxBlocks, (rows + 3) / 4));
+  hipLaunchKernelGGL(minmax_kernel, dim3(blocks), dim3(256), 0, s, x, ldx, rows, width, row_map, row_edge, in_left,
+                     in_right, static_cast<float2 *>(part));
+  hipLaunchKernelGGL(params_kernel, dim3(1), dim3(256), 0, s, static_cast<const float2 *>(part), blocks,
+                     static_cast<QP *>(params));
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
+size_t i8_params_scratch_bytes() { return sizeof(float2) * kMinmaxBlocks + 256; }
+
+int launch_i8_quantize(hipStream_t s, const float *x, int ldx, int rows, int width, const int *row_map, int nseg,
+                       const int *offs, const void *params, int8_t *q, int ldq, int32_t *rowsum) {
+  SpliceOffsets so = {};
+  for (int i = 0; i < nseg; ++i) so.off[i] = offs[i];
+  if (rows > 0)
+    hipLaunchKernelGGL(quantize_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, ldx, rows, width, row_map, nseg,
+                       so, static_cast<const QP *>(params), q, ldq, rowsum);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
+int launch_i8_gemm(hipStream_t s, const I8Layer &L, const int8_t *a, int lda, int m, const int32_t *rowsum,
+                   const void *pa, float *y, int ldy) {
+  I8Args p = {};
+  p.a = a;
+  p.lda = lda;
+  p.m = m;
+  p.din = L.a_din;
+  p.nseg = L.a_nseg;
+  for (int i = 0; i < 8; ++i) p.off[i] = L.a_off[i];
+  p.rowsum = rowsum;
+  p.w = L.wq.as<int8_t>();
+  p.colsum = L.colsum.as<int32_t>();
+  p.n = L.n;
+  p.k = L.k;
+  p.kpad = L.kpad;
+  p.pa = pa;
+  p.w_scale = L.w_scale;
+  p.w_zp = L.w_zp;
+  p.bias = L.bias;
+  p.bn_scale = L.bn_scale;
+  p.bn_offset = L.bn_offset;
+  for (int i = 0; i < 4; ++i) p.post[i] = L.post[i];
+  p.npost = L.npost;
+  p.y = y;
+  p.ldy = ldy;
+  static const int use_glds = [] {
+    const char *e = getenv("CATEARS_I8_GEMM");
+    return e ? atoi(e) : 1;
+  }();
+  if (use_glds && p.kpad % 128 == 0 && p.din % 128 == 0 && lda % 16 == 0) {
+    auto go = [&](auto kern, int bm, int bn) {
+      p.tiles_n = (L.n + bn - 1) / bn;
+      p.tiles_m = (m + bm - 1) / bm;
+      p.group = 8;  // an XCD's tiles: 8 column tiles x its row blocks
+      hipLaunchKernelGGL(kern, dim3(p.tiles_m * p.tiles_n), dim3(256), 0, s, p);
+    };
+    switch (use_glds) {
+      case 2: go(gemm_i8_glds_kernel<128, 128, 3>, 128, 128); break;
+      case 3: go(gemm_i8_glds_kernel<128, 128, 4>, 128, 128); break;
+      case 4: go(gemm_i8_glds_kernel<128, 64, 4>, 128, 64); break;
+      case 5: go(gemm_i8_glds_kernel<64, 128, 4>, 64, 128); break;
+      case 6: go(gemm_i8_glds_kernel<128, 64, 3>, 128, 64); break;
+      default: go(gemm_i8_glds_kernel<128, 128, 2>, 128, 128); break;
+    }
+    CE_HIP(hipGetLastError());
+    return CE_GPU_OK;
+  }
+  p.tiles_n = (L.n + IBN - 1) / IBN;
+  if (p.kpad % IBK != 0 || (p.nseg > 1 && p.din % IBK != 0) || lda % 16 != 0)
+    return fail(CE_GPU_EINVAL, "gemm_i8_nnet: bad K geometry");
+  const int tiles_m = (m + IBM - 1) / IBM;
+  hipLaunchKernelGGL(gemm_i8_nnet_kernel, dim3(tiles_m * p.tiles_n), dim3(256), 0, s, p);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
+int i8_k_align() { return 128; }  // the LDS-DMA kernel's K-tile (bytes)
+
+}  // namespace catears

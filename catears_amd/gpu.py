@@ -28,7 +28,7 @@ ABI = [
     "ce_gpu_am_forward", "ce_gpu_score", "ce_gpu_sgemm", "ce_gpu_quantize",
     "ce_gpu_gemm_u8u8f32", "ce_gpu_gemm_u8u8i32", "ce_gpu_model_load_mem",
     "ce_gpu_nnet_propagate", "ce_gpu_linear", "ce_gpu_splice", "ce_gpu_rowwise",
-    "ce_gpu_profile_anchor", "ce_gpu_ctx_profile_intervals",
+    "ce_gpu_profile_anchor", "ce_gpu_ctx_profile_intervals", "ce_gpu_model_quantize",
 ]
 
 _lib = None
@@ -79,6 +79,7 @@ def lib():
         "ce_gpu_gemm_u8u8f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp]),
         "ce_gpu_gemm_u8u8i32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp]),
         "ce_gpu_profile_anchor": (ci, [ci, vp]),
+        "ce_gpu_model_quantize": (ci, [vp, vp]),
         "ce_gpu_ctx_profile_intervals": (ci, [vp, ci, vp, vp, ci, pi]),
         "ce_gpu_model_load_mem": (ci, [vp, vp, i64, vp, ci, ci, ci, pp]),
         "ce_gpu_nnet_propagate": (ci, [vp, vp, vp, ci, ci, ci, vp]),
@@ -128,7 +129,7 @@ class Context:
     def synchronize(self):
         check(lib().ce_gpu_ctx_synchronize(self.h))
 
-    PROF_GEMM, PROF_GEMM_GATHER, PROF_FBANK, PROF_CMVN, PROF_FINALIZE = range(5)
+    PROF_GEMM, PROF_GEMM_GATHER, PROF_FBANK, PROF_CMVN, PROF_FINALIZE, PROF_QUANT = range(6)
 
     def profile(self, enable=True):
         check(lib().ce_gpu_ctx_profile(self.h, int(enable)))
@@ -187,6 +188,11 @@ class Model:
         check(lib().ce_gpu_model_info(h, *[ctypes.byref(x) for x in v], ctypes.byref(p)))
         self.left, self.right, self.input_dim, self.num_pdfs, self.num_linear = [x.value for x in v]
         self.num_params = p.value
+
+    def quantize(self, ctx):
+        """Switch to the int8 path (ce_gpu_model_quantize)."""
+        check(lib().ce_gpu_model_quantize(ctx.h, self.h))
+        return self
 
     def tid2pdf(self):
         n = ctypes.c_int()

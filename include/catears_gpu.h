@@ -84,7 +84,8 @@ int ce_gpu_ctx_synchronize(ce_gpu_ctx *ctx);
 #define CE_GPU_PROF_FBANK 2
 #define CE_GPU_PROF_CMVN 3
 #define CE_GPU_PROF_FINALIZE 4
-#define CE_GPU_PROF_CLASSES 5
+#define CE_GPU_PROF_QUANT 5 /* int8 path: per-layer min/max + quantize passes */
+#define CE_GPU_PROF_CLASSES 6
 int ce_gpu_ctx_profile(ce_gpu_ctx *ctx, int enable);
 int ce_gpu_ctx_profile_read(ce_gpu_ctx *ctx, int kernel_class, double *total_ms, int64_t *launches);
 
@@ -116,6 +117,16 @@ int ce_gpu_model_load(ce_gpu_ctx *ctx, const char *nnet_path, const char *prior_
 /* Shape of a loaded model.  Any output pointer may be NULL. */
 int ce_gpu_model_info(const ce_gpu_model *m, int *left_context, int *right_context,
                       int *input_dim, int *num_pdfs, int *num_linear, int64_t *num_params);
+
+/* Switch a loaded model to the int8 path (BASELINE config C5): every
+ * LinearLayer becomes Quantize + MatMat_U8U8F32 + bias (src/matrix.cc:329-420
+ * -- the pieces the reference ships but never wires into Nnet,
+ * src/nnet.cc:29).  Weights are quantized once here, per tensor; activations
+ * per layer and per chunk of packed rows (the layer input block, before the
+ * splice -- the same parameters as quantizing the spliced block); the int32
+ * accumulation is exact (gemmlowp's ring), bias / ReLU / BatchNorm /
+ * LogSoftmax stay fp32.  Irreversible for this model handle. */
+int ce_gpu_model_quantize(ce_gpu_ctx *ctx, ce_gpu_model *m);
 
 /* tid2pdf map (AcousticModel::TransitionPdfIdMap, src/am.h:38-40).  Copies
  * min(capacity, size) ints to h_out and returns the size via *size. */

@@ -488,17 +488,23 @@ ORC_EXPORT void orc_quant_params(long count, const float *x, float *scale_out, i
   *scale_out = (float)scale;
 }
 
+/* The elementwise step of Quantize (src/matrix.cc:378-386):
+ * std::max(0.0f, std::min(val, 255.0f)) spelled out as the standard library
+ * defines it -- min(a, b) = (b < a) ? b : a, max(a, b) = (a < b) ? b : a --
+ * so a NaN input becomes 0. */
+ORC_EXPORT void orc_quantize_apply(long count, const float *x, float scale, int32_t zp, uint8_t *q) {
+  for (long i = 0; i < count; ++i) {
+    float v = x[i] / scale + (float)zp;
+    v = (255.0f < v) ? 255.0f : v;
+    v = (0.0f < v) ? v : 0.0f;
+    q[i] = (uint8_t)roundf(v);
+  }
+}
+
 ORC_EXPORT void orc_quantize(long count, const float *x, uint8_t *q, float *scale_out,
                              int32_t *zp_out) {
   orc_quant_params(count, x, scale_out, zp_out);
-  float scale = *scale_out;
-  int32_t zp = *zp_out;
-  for (long i = 0; i < count; ++i) {
-    float v = x[i] / scale + (float)zp;
-    v = v < 255.0f ? v : 255.0f;
-    v = 0.0f > v ? 0.0f : v;
-    q[i] = (uint8_t)roundf(v);
-  }
+  orc_quantize_apply(count, x, *scale_out, *zp_out, q);
 }
 
 /* C[i][j] = float(int32( sum_k (A[i][k]-zpA)(B[k][j]-zpB) )) * (sA*sB).

@@ -55,6 +55,7 @@ def lib():
                                        ctypes.POINTER(ctypes.c_int32)]
         L.orc_quantize.argtypes = [cl, f32p, u8p, ctypes.POINTER(ctypes.c_float),
                                    ctypes.POINTER(ctypes.c_int32)]
+        L.orc_quantize_apply.argtypes = [cl, f32p, ctypes.c_float, ctypes.c_int32, u8p]
         L.orc_gemm_u8u8_i32.argtypes = [ci, ci, ci, u8p, ctypes.c_int32, u8p, ctypes.c_int32, i32p]
         L.orc_gemm_u8u8f32.argtypes = [ci, ci, ci, u8p, ctypes.c_float, ctypes.c_int32,
                                        u8p, ctypes.c_float, ctypes.c_int32, f32p]
@@ -204,6 +205,43 @@ def nnet_propagate(layers, x, gemm=None):
     for layer in layers:
         x = layer_forward(layer, x, gemm)
     return x
+
+
+def nnet_propagate_int8(layers, x):
+    """Nnet::Propagate with every LinearLayer as Quantize + MatMat_U8U8F32 +
+    bias (src/matrix.cc:329-420) -- the int8 path of BASELINE config C5, as
+    catears_amd runs it (include/catears_gpu.h ce_gpu_model_quantize): the
+    activation parameters come from the block entering the Splice (equal to
+    those of the spliced block, whose rows it all reads), weights per tensor."""
+    x = np.ascontiguousarray(x, np.float32)
+    pre = None  # block entering the pending Splice
+    for layer in layers:
+        kind = layer["kind"]
+        if kind == "splice":
+            pre = x
+            x = layer_forward(layer, x)
+        elif kind == "linear":
+            src = pre if pre is not None else x
+            _, sx, zx = quantize(src)
+            xq = _quantize_with(x, sx, zx)
+            wq, sw, zw = quantize(layer["W"])
+            y = gemm_u8u8f32(xq, sx, zx, wq, sw, zw)
+            x = (y + np.asarray(layer["b"], np.float32)[None, :]).astype(np.float32)
+            pre = None
+        else:
+            x = layer_forward(layer, x)
+            if kind != "narrow":
+                pre = None
+    return x
+
+
+def _quantize_with(x, scale, zp):
+    """Quantize's elementwise step with given parameters (matrix.cc:378-386)."""
+    x = np.ascontiguousarray(x, np.float32)
+    q = np.zeros(x.shape, np.uint8)
+    if x.size:
+        lib().orc_quantize_apply(x.size, x.reshape(-1), scale, zp, q.reshape(-1))
+    return q
 
 
 def am_stream(model, feats, chunk_size=50, gemm=None):
