@@ -315,19 +315,20 @@ __global__ __launch_bounds__(256, 2) void gemm_i8_nnet_kernel(I8Args p) {
 // A 32x32x32 i8 MFMA operand is one ds_read_b128 per lane (row r, bytes
 // 16h..16h+15 of its 32-byte k-step), so a tile row of 128 bytes holds the
 // four k-steps of the tile.  BM x BN block tile, 2 x 2 waves.
-template <int BM, int BN, int STAGES>
-__global__ __launch_bounds__(256, 1) void gemm_i8_glds_kernel(I8Args p) {
+template <int BM, int BN, int STAGES, int WGM = 2, int WGN = 2>
+__global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_i8_glds_kernel(I8Args p) {
+  constexpr int NW = WGM * WGN;
   constexpr int BKB = 128;                  // bytes per K-tile row
-  constexpr int TI = BM / 2 / 32, TJ = BN / 2 / 32;
+  constexpr int TI = BM / WGM / 32, TJ = BN / WGN / 32;
   constexpr int RPI = 1024 / BKB;           // rows per DMA instruction (8)
-  constexpr int NGA = BM * BKB / 1024 / 4, NGB = BN * BKB / 1024 / 4;
+  constexpr int NGA = BM * BKB / 1024 / NW, NGB = BN * BKB / 1024 / NW;
   constexpr int STAGE = (BM + BN) * BKB;    // bytes
-  static_assert(NGA >= 1 && NGB >= 1, "tile too small");
+  static_assert(NGA >= 1 && NGB >= 1 && TI >= 1 && TJ >= 1, "tile too small");
   __shared__ __attribute__((aligned(1024))) int8_t smem[STAGES * STAGE];
   auto swz = [](int row) { return (row >> 1) & 7; };
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1, r = lane & 31, h = lane >> 5;
+  const int wm = wave / WGN, wn = wave % WGN, r = lane & 31, h = lane >> 5;
   int tm, tn;
   tile_of(blockIdx.x, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
   const int m0 = tm * BM, n0 = tn * BN;
@@ -505,14 +506,14 @@ int launch_i8_gemm(hipStream_t s, const I8Layer &L, const int8_t *a, int lda, in
   p.ldy = ldy;
   static const int use_glds = [] {
     const char *e = getenv("CATEARS_I8_GEMM");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 9;  // measured best on TDNN-S, frame batch 8192 (scratch sweep)
   }();
   if (use_glds && p.kpad % 128 == 0 && p.din % 128 == 0 && lda % 16 == 0) {
-    auto go = [&](auto kern, int bm, int bn) {
+    auto go = [&](auto kern, int bm, int bn, int threads = 256) {
       p.tiles_n = (L.n + bn - 1) / bn;
       p.tiles_m = (m + bm - 1) / bm;
       p.group = 8;  // an XCD's tiles: 8 column tiles x its row blocks
-      hipLaunchKernelGGL(kern, dim3(p.tiles_m * p.tiles_n), dim3(256), 0, s, p);
+      hipLaunchKernelGGL(kern, dim3(p.tiles_m * p.tiles_n), dim3(threads), 0, s, p);
     };
     switch (use_glds) {
       case 2: go(gemm_i8_glds_kernel<128, 128, 3>, 128, 128); break;
@@ -520,6 +521,12 @@ int launch_i8_gemm(hipStream_t s, const I8Layer &L, const int8_t *a, int lda, in
       case 4: go(gemm_i8_glds_kernel<128, 64, 4>, 128, 64); break;
       case 5: go(gemm_i8_glds_kernel<64, 128, 4>, 64, 128); break;
       case 6: go(gemm_i8_glds_kernel<128, 64, 3>, 128, 64); break;
+      case 7: go(gemm_i8_glds_kernel<256, 128, 2, 4, 2>, 256, 128, 512); break;
+      // 9: 256 x 256 tiles, 8 waves of 64 x 128: twice the MFMA work per
+      // K-tile iteration of the 128 x 128 form -- the loop is bound by the
+      // DMA round trip per iteration, not by MFMA issue
+      case 8: go(gemm_i8_glds_kernel<128, 256, 2, 2, 4>, 128, 256, 512); break;
+      case 9: go(gemm_i8_glds_kernel<256, 256, 2, 4, 2>, 256, 256, 512); break;
       default: go(gemm_i8_glds_kernel<128, 128, 2>, 128, 128); break;
     }
     CE_HIP(hipGetLastError());
