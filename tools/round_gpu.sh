@@ -26,3 +26,19 @@ for grp in FETCH_SIZE WRITE_SIZE; do
   echo "pmc pass $i ok: $grp"
 done
 python "$R/tools/pmc_traffic.py" "$OUT/pmc1" "$OUT/pmc2" "$OUT/pmc_traffic.json"
+[ -n "$SKIP_EXTRA" ] && exit 0
+# secondary workloads: C2 (batched fbank) and C5 (int8 nnet), same recipe
+for W in c2 c5; do
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$W" -o run -- \
+      python "$R/bench.py" --workload $W --steps ${STEPS_EXTRA:-30} --warmup 3 > "$OUT/bench_$W.log" 2>&1 || { echo "bench $W failed"; tail -20 "$OUT/bench_$W.log"; exit 1; }
+  echo "bench $W ok"; grep '^{' "$OUT/bench_$W.log" | cut -c1-300
+  case $W in c2) KRE="fbank";; c5) KRE="gemm_i8|quantize|minmax";; esac
+  i=0
+  for grp in FETCH_SIZE WRITE_SIZE; do
+    i=$((i+1))
+    timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "$KRE" --output-format csv -d "$OUT/pmc_${W}_$i" -o run -- \
+        python "$R/bench.py" --workload $W --steps 3 --warmup 1 --no-cpu-baseline --no-profile --serial \
+        > "$OUT/pmc_${W}_$i.log" 2>&1 || { echo "pmc $W $i failed"; tail -20 "$OUT/pmc_${W}_$i.log"; exit 1; }
+  done
+  python "$R/tools/pmc_traffic.py" "$OUT/pmc_${W}_1" "$OUT/pmc_${W}_2" "$OUT/pmc_traffic_$W.json"
+done
