@@ -71,6 +71,11 @@ $(PKTEST): tests/native/pk_dropin.cc $(PKLIB) $(PKHDRS)
 	$(CXX) $(PKFLAGS) -o $@ $< -Lcatears_amd/lib -lcatears_pk -lcatears_hip -L/opt/rocm/lib -lamdhip64 \
 	    -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,/opt/rocm/lib
 
-host: $(PKLIB) $(PKTEST)
+COMPATTEST := build/bin/compat_test
+$(COMPATTEST): tests/native/compat_test.cc $(wildcard $(HOST)/compat_src/*.cc) $(wildcard $(HOST)/compat/*.h)
+	@mkdir -p $(dir $@)
+	$(CXX) -O1 -std=c++17 -Wall -I$(HOST)/compat -o $@ $< $(wildcard $(HOST)/compat_src/*.cc)
+
+host: $(PKLIB) $(PKTEST) $(COMPATTEST)
 all: host
 .PHONY: host

@@ -95,6 +95,16 @@ def test_dropin_library_exports_the_reference_api():
         assert sym in out, sym
 
 
+def test_compat_container_layer(tmp_path):
+    """The stand-ins for the reference's container headers: Configuration,
+    VEC0 / MAT0 readers and their error strings (no GPU)."""
+    exe = os.path.join(ROOT, "build", "bin", "compat_test")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "-C", ROOT, "build/bin/compat_test"], stdout=subprocess.DEVNULL)
+    r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True)
+    assert r.returncode == 0 and "PASSED" in r.stdout, r.stdout + r.stderr
+
+
 # ------------------------------------------------------------ GPU checks --
 
 def _run(*args):
