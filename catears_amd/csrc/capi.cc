@@ -794,6 +794,15 @@ int ce_gpu_cmvn(ce_gpu_ctx *ctx, const ce_gpu_plan *p, const float *d_global_sta
 }  // extern "C"
 
 namespace catears {
+// CATEARS_SPLICE_FIRST=0 keeps the gather loader for narrow segments (A/B).
+static bool splice_first_layer() {
+  static const bool on = [] {
+    const char *e = getenv("CATEARS_SPLICE_FIRST");
+    return !e || atoi(e) != 0;
+  }();
+  return on;
+}
+
 // Runs the program's steps on `rows` packed rows starting at x (row_map: the
 // first layer's packed row -> source row, or NULL for identity).  Returns the
 // last activation via *y / *ldy.
@@ -829,6 +838,21 @@ static int run_steps_f32(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
       a.ldy = g.n;
       {
         ProfScope prof(ctx, g.din % 32 == 0 ? CE_GPU_PROF_GEMM : CE_GPU_PROF_GEMM_GATHER);
+        if (g.din % 32 != 0 && splice_first_layer()) {
+          // Segments narrower than a K-tile (the 40-wide first layer):
+          // write the spliced block once (rows x kpad, zero padded) and run
+          // the fast kernel on it -- cheaper than a per-element gather loader.
+          CE_TRY(ensure_scratch(ctx, (size_t)rows * g.kpad * sizeof(float)));
+          float *xs = static_cast<float *>(ctx->scratch.ptr);
+          CE_TRY(launch_splice_pad(ctx->stream, x, ldx, rows, g.din, g.nseg, g.off, a.row_map, xs, g.kpad));
+          a.x = xs;
+          a.ldx = g.kpad;
+          a.row_map = nullptr;
+          a.k = g.kpad;  // the padding columns are zero on both sides
+          a.din = g.kpad;
+          a.nseg = 1;
+          for (int i = 0; i < 8; ++i) a.off[i] = 0;
+        }
         CE_TRY(launch_gemm_f32(ctx->stream, a));
       }
       x = buf[cur];

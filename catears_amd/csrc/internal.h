@@ -251,6 +251,10 @@ int launch_rowop_raw(hipStream_t s, int kind, int dim, const float *scale, const
                      int ldx, int rows);
 int launch_splice(hipStream_t s, int rows, int dim, const float *in, int ld_in, const int32_t *h_idx,
                   int n_idx, float *out);
+// out[r][s*din + c] = in[row_map(clamp(r + off[s]))][c], zero for columns
+// nseg*din .. ldo-1 (the fused program's first-layer block).
+int launch_splice_pad(hipStream_t s, const float *in, int ld_in, int rows, int din, int nseg, const int *off,
+                      const int *row_map, float *out, int ldo);
 
 int launch_quantize(hipStream_t s, const float *x, int64_t count, uint8_t *q, void *params,
                     void *scratch);

@@ -128,7 +128,37 @@ __global__ __launch_bounds__(256) void splice_kernel(int rows, int dim, const fl
   }
 }
 
+__global__ __launch_bounds__(256) void splice_pad_kernel(const float *__restrict__ in, int ld_in, int rows, int din,
+                                                         int nseg, SpliceIdx idx, const int *__restrict__ row_map,
+                                                         float *__restrict__ out, int ldo) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  float *o = out + (int64_t)r * ldo;
+  for (int c = lane; c < ldo; c += 64) {
+    const int s = c / din;
+    float v = 0.0f;
+    if (s < nseg) {
+      int src = r + idx.v[s];
+      src = src < 0 ? 0 : (src > rows - 1 ? rows - 1 : src);
+      if (row_map) src = row_map[src];
+      v = in[(int64_t)src * ld_in + (c - s * din)];
+    }
+    o[c] = v;
+  }
+}
+
 }  // namespace
+
+int launch_splice_pad(hipStream_t s, const float *in, int ld_in, int rows, int din, int nseg, const int *off,
+                      const int *row_map, float *out, int ldo) {
+  SpliceIdx idx = {};
+  for (int i = 0; i < nseg && i < CE_GPU_MAX_SPLICE; ++i) idx.v[i] = off[i];
+  if (rows > 0)
+    hipLaunchKernelGGL(splice_pad_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, in, ld_in, rows, din, nseg, idx,
+                       row_map, out, ldo);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
 
 int launch_splice(hipStream_t s, int rows, int dim, const float *in, int ld_in, const int32_t *h_idx,
                   int n_idx, float *out) {
