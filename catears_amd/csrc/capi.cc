@@ -1042,6 +1042,51 @@ int ce_gpu_nnet_propagate(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *d
                          d_out);
 }
 
+int ce_gpu_nnet_propagate_blocks(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *d_in, int ld_in,
+                                 const int32_t *h_rows, int n_blocks, int subtract_prior, float *d_out) {
+  if (!ctx || !m || !d_in || !d_out || !h_rows || n_blocks < 1) return fail(CE_GPU_EINVAL, "bad argument");
+  if (ld_in < m->input_dim) return fail(CE_GPU_EINVAL, "ld_in smaller than the nnet input");
+  if (subtract_prior && !m->log_prior.ptr) return fail(CE_GPU_EINVAL, "model has no prior");
+  const int L = m->net_left, R = m->net_right;
+  int64_t total = 0;
+  for (int b = 0; b < n_blocks; ++b) {
+    if (h_rows[b] <= L + R)
+      return fail(CE_GPU_EINVAL, fmt("nnet_propagate_blocks: block %d has %d rows, context is (%d, %d)", b,
+                                     h_rows[b], L, R));
+    total += h_rows[b];
+  }
+  if (total >= INT32_MAX / 2) return fail(CE_GPU_EINVAL, "too many rows");
+  const int rows = (int)total;
+  // per packed row: output row (or -1) and distances to its block's edges;
+  // written only after the previous call's kernels are done with them
+  CE_HIP(hipStreamSynchronize(ctx->stream));
+  ctx->h_blk_maps.resize(2 * (size_t)rows);
+  int32_t *dst = ctx->h_blk_maps.data();
+  uint32_t *edge = reinterpret_cast<uint32_t *>(dst + rows);
+  int r = 0, out = 0;
+  for (int b = 0; b < n_blocks; ++b) {
+    const int n = h_rows[b];
+    for (int j = 0; j < n; ++j, ++r) {
+      dst[r] = (j >= L && j < n - R) ? out++ : -1;
+      const uint32_t dl = (uint32_t)std::min(j, 0xffff), dr = (uint32_t)std::min(n - 1 - j, 0xffff);
+      edge[r] = dl | (dr << 16);
+    }
+  }
+  const size_t bytes = ctx->h_blk_maps.size() * 4;
+  if (ctx->blk_maps.bytes < bytes) CE_TRY(ctx->blk_maps.alloc(bytes));
+  CE_HIP(hipMemcpyAsync(ctx->blk_maps.ptr, ctx->h_blk_maps.data(), bytes, hipMemcpyHostToDevice, ctx->stream));
+  const int32_t *d_dst = ctx->blk_maps.as<int32_t>();
+  const uint32_t *d_edge = reinterpret_cast<const uint32_t *>(d_dst + rows);
+  const float *y = nullptr;
+  int ldy = 0;
+  // blocks are independent: the rows a Splice reads across a block boundary
+  // only feed rows that block's Narrow drops
+  CE_TRY(run_steps(ctx, m, d_in, ld_in, rows, nullptr, d_edge, &y, &ldy));
+  ProfScope prof(ctx, CE_GPU_PROF_FINALIZE);
+  return launch_finalize(ctx->stream, y, ldy, rows, m->num_pdfs, m->final_log_softmax,
+                         subtract_prior ? m->log_prior.as<float>() : nullptr, d_dst, d_out);
+}
+
 int ce_gpu_score(ce_gpu_ctx *ctx, const ce_gpu_model *m, const ce_gpu_plan *p, const float *d_pcm,
                  const float *d_global_stats, float *d_feats_ws, float *d_loglik) {
   if (!ctx || !m || !p) return fail(CE_GPU_EINVAL, "NULL argument");

@@ -160,6 +160,8 @@ struct ce_gpu_ctx {
   catears::DevBuf workspace;   // nnet activations (grown on demand)
   size_t workspace_floats = 0;
   catears::DevBuf scratch;     // reductions / int8 operand staging (grown on demand)
+  catears::DevBuf blk_maps;    // ce_gpu_nnet_propagate_blocks: row_dst + row_edge
+  std::vector<int32_t> h_blk_maps;
   // optional per-class launch timing (ce_gpu_ctx_profile)
   bool profiling = false;
   struct Timed {

@@ -617,7 +617,7 @@ __device__ __forceinline__ void glds16(const char *src, float *lds_dst) {
                                    (__attribute__((address_space(3))) void *)lds_dst, 16, 0, 0);
 }
 
-template <class C, int STAGES>
+template <class C, int STAGES, bool PRIO = false>
 __global__ __launch_bounds__(C::NT, 1) void gemm_f32_glds_kernel(KArgs p) {
   constexpr int BM = C::BM, BN = C::BN, BK = C::BK, TI = C::TI, TJ = C::TJ, NW = C::NW;
   static_assert(BK == 32 || BK == 64, "tile rows of 128 or 256 bytes");
@@ -719,11 +719,13 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_f32_glds_kernel(KArgs p) {
     const float *st = smem + (kt % STAGES) * STAGE;
     f32x4 fa0[TI], fb0[TJ], fa1[TI], fb1[TJ];
     frag(st, 0, fa0, fb0);
+    if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int g = 0; g < BK / 8; ++g) {
       if (g + 1 < BK / 8) frag(st, g + 1, (g & 1) ? fa0 : fa1, (g & 1) ? fb0 : fb1);
       mma((g & 1) ? fa1 : fa0, (g & 1) ? fb1 : fb0);
     }
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
   }
 
 #pragma unroll
@@ -757,13 +759,13 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_f32_glds_kernel(KArgs p) {
 
 // glds for the layers it fits, pipe2 for the rest (first layer's gather,
 // N-major MatMat operands).
-template <class C, int STAGES = 3>
+template <class C, int STAGES = 3, bool PRIO = false>
 int launch_glds(hipStream_t s, KArgs p, bool a_fast, bool b_nmajor, bool rm) {
   if (!(a_fast && !b_nmajor && !rm && p.din % C::BK == 0 && p.kpad % C::BK == 0))
     return launch_pipe2<V3>(s, p, a_fast, b_nmajor, rm);
   p.tiles_n = (p.n + C::BN - 1) / C::BN;
   p.tiles_m = (p.m + C::BM - 1) / C::BM;
-  hipLaunchKernelGGL((gemm_f32_glds_kernel<C, STAGES>), dim3(p.tiles_m * p.tiles_n), dim3(C::NT), 0, s, p);
+  hipLaunchKernelGGL((gemm_f32_glds_kernel<C, STAGES, PRIO>), dim3(p.tiles_m * p.tiles_n), dim3(C::NT), 0, s, p);
   CE_HIP(hipGetLastError());
   return CE_GPU_OK;
 }
@@ -899,6 +901,10 @@ int launch_gemm_f32(hipStream_t s, const GemmArgs &a) {
       return launch_glds<W6, 2>(s, p, a_fast, a.b_nmajor, rm);
     case 34:
       return launch_glds<V0, 2>(s, p, a_fast, a.b_nmajor, rm);
+    case 36:
+      return launch_glds<V2, 2, true>(s, p, a_fast, a.b_nmajor, rm);
+    case 37:
+      return launch_glds<V2, 3, true>(s, p, a_fast, a.b_nmajor, rm);
     case 35:
       return deep ? launch_glds<V1, 2>(s, p, a_fast, a.b_nmajor, rm) : launch_glds<V0, 2>(s, p, a_fast, a.b_nmajor, rm);
     default:

@@ -29,6 +29,7 @@ ABI = [
     "ce_gpu_gemm_u8u8f32", "ce_gpu_gemm_u8u8i32", "ce_gpu_model_load_mem",
     "ce_gpu_nnet_propagate", "ce_gpu_linear", "ce_gpu_splice", "ce_gpu_rowwise",
     "ce_gpu_profile_anchor", "ce_gpu_ctx_profile_intervals", "ce_gpu_model_quantize",
+    "ce_gpu_nnet_propagate_blocks",
 ]
 
 _lib = None
@@ -80,6 +81,7 @@ def lib():
         "ce_gpu_gemm_u8u8i32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp]),
         "ce_gpu_profile_anchor": (ci, [ci, vp]),
         "ce_gpu_model_quantize": (ci, [vp, vp]),
+        "ce_gpu_nnet_propagate_blocks": (ci, [vp, vp, vp, ci, ctypes.POINTER(ctypes.c_int32), ci, ci, vp]),
         "ce_gpu_ctx_profile_intervals": (ci, [vp, ci, vp, vp, ci, pi]),
         "ce_gpu_model_load_mem": (ci, [vp, vp, i64, vp, ci, ci, ci, pp]),
         "ce_gpu_nnet_propagate": (ci, [vp, vp, vp, ci, ci, ci, vp]),
@@ -310,6 +312,19 @@ def nnet_propagate(ctx, model, x, subtract_prior=False, out=None):
     if out is None:
         out = torch.empty((max(rows - net_l - net_r, 0), model.num_pdfs), dtype=torch.float32, device=x.device)
     check(lib().ce_gpu_nnet_propagate(ctx.h, model.h, _ptr(x), rows, x.stride(0), int(subtract_prior), _ptr(out)))
+    return out
+
+
+def nnet_propagate_blocks(ctx, model, x, block_rows, subtract_prior=False, out=None):
+    """ce_gpu_nnet_propagate_blocks: independent padded blocks back to back."""
+    import torch
+    rows = np.ascontiguousarray(block_rows, np.int32)
+    n_out = int(rows.sum()) - len(rows) * (model.left + model.right)
+    if out is None:
+        out = torch.empty((n_out, model.num_pdfs), dtype=torch.float32, device=x.device)
+    check(lib().ce_gpu_nnet_propagate_blocks(ctx.h, model.h, _ptr(x), x.stride(0),
+                                             rows.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), len(rows),
+                                             int(subtract_prior), _ptr(out)))
     return out
 
 

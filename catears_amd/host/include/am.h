@@ -8,9 +8,17 @@
 // Because every Splice is followed by its Narrow, a batch's rows do not
 // depend on where chunks start, so a larger chunk_size in the config only
 // changes how many rows one device call carries.
+//
+// Serving many streams: with the optional config key
+// gpu_batch_streams = N > 1, chunks that become ready on different Instances
+// (threads) at about the same time are scored in ONE device call
+// (ce_gpu_nnet_propagate_blocks): the first caller waits up to
+// gpu_batch_wait_us (default 200) for up to N-1 others, runs the batch, and
+// every caller gets exactly the rows it would have got alone.
 #ifndef CATEARS_PK_AM_H_
 #define CATEARS_PK_AM_H_
 
+#include <memory>
 #include <vector>
 
 #include "catears_runtime.h"
@@ -48,7 +56,11 @@ class AcousticModel {
   // Device program (for batch scorers built on the same model).
   const ce_gpu_model *device_model() const { return model_; }
 
+  // Device calls made so far / blocks they carried (batching statistics).
+  void batch_stats(int64_t *calls, int64_t *blocks) const;
+
  private:
+  struct Batcher;
   ce_gpu_model *model_ = nullptr;
   int left_context_ = 0;
   int right_context_ = 0;
@@ -56,9 +68,12 @@ class AcousticModel {
   int num_pdfs_ = 0;
   int feat_dim_ = 0;
   Vector<int32_t> tid2pdf_;
+  std::unique_ptr<Batcher> batcher_;
 
   void Append(Instance *inst, const float *frame, int dim) const;
   void ComputeBatch(Instance *inst, int batch_size, Matrix<float> *log_prob) const;
+  void RunBlocks(const std::vector<const float *> &rows, const std::vector<int32_t> &n, int dim,
+                 const std::vector<Matrix<float> *> &out) const;
   AcousticModel(const AcousticModel &) = delete;
   AcousticModel &operator=(const AcousticModel &) = delete;
 };

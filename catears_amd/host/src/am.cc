@@ -4,17 +4,51 @@
 #include <assert.h>
 #include <string.h>
 
+#include <chrono>
+#include <condition_variable>
 #include <memory>
+#include <mutex>
 
 namespace pocketkaldi {
 
 using catears::host::Check;
 using catears::host::Runtime;
 
+// Leader/follower batching of ready chunks across Instances: whoever finds
+// no batch in progress leads -- waits for up to `max_blocks` requests or
+// `wait`, runs them as one device call, marks them done; a request left
+// behind by a finished batch makes its owner the next leader.
+struct AcousticModel::Batcher {
+  struct Req {
+    Req(const float *r, int n_, int d, Matrix<float> *o) : rows(r), n(n_), dim(d), out(o), done(false) {}
+    const float *rows;
+    int n, dim;
+    Matrix<float> *out;
+    bool done;
+  };
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<Req *> pending;
+  bool leader_active = false;
+  int max_blocks = 1;
+  std::chrono::microseconds wait{200};
+  int64_t calls = 0, blocks = 0;
+};
+
 AcousticModel::AcousticModel() {}
 
 AcousticModel::~AcousticModel() {
   if (model_) ce_gpu_model_destroy(model_);
+}
+
+void AcousticModel::batch_stats(int64_t *calls, int64_t *blocks) const {
+  if (!batcher_) {
+    *calls = *blocks = 0;
+    return;
+  }
+  std::lock_guard<std::mutex> lk(batcher_->mu);
+  *calls = batcher_->calls;
+  *blocks = batcher_->blocks;
 }
 
 Status AcousticModel::Read(const Configuration &conf) {
@@ -59,6 +93,9 @@ Status AcousticModel::Read(const Configuration &conf) {
   if (rc != CE_GPU_OK) return Status::Corruption(util::Format("{}: {}", nnet_file, ce_gpu_last_error()));
   int pdfs = 0;
   ce_gpu_model_info(model_, nullptr, nullptr, &feat_dim_, &pdfs, nullptr, nullptr);
+  batcher_.reset(new Batcher());
+  batcher_->max_blocks = conf.GetIntegerOrElse("gpu_batch_streams", 1);
+  batcher_->wait = std::chrono::microseconds(conf.GetIntegerOrElse("gpu_batch_wait_us", 200));
   return Status::OK();
 }
 
@@ -86,17 +123,76 @@ void AcousticModel::ComputeBatch(Instance *inst, int batch_size, Matrix<float> *
   assert((int)inst->size() >= rows_in && "ComputeBatch: insufficient data");
   const int dim = inst->dim;
   if (dim != feat_dim_) throw catears::host::DeviceError("AcousticModel: feature width differs from the nnet input");
+  const float *rows = inst->rows.data() + inst->head * dim;
+  if (batcher_ && batcher_->max_blocks > 1) {
+    Batcher &b = *batcher_;
+    Batcher::Req req(rows, rows_in, dim, log_prob);
+    std::unique_lock<std::mutex> lk(b.mu);
+    b.pending.push_back(&req);
+    b.cv.notify_all();
+    while (!req.done) {
+      if (!b.leader_active) {
+        b.leader_active = true;
+        b.cv.wait_for(lk, b.wait, [&] { return (int)b.pending.size() >= b.max_blocks; });
+        std::vector<Batcher::Req *> batch;
+        batch.swap(b.pending);
+        lk.unlock();
+        std::vector<const float *> ptrs;
+        std::vector<int32_t> ns;
+        std::vector<Matrix<float> *> outs;
+        for (Batcher::Req *q : batch) ptrs.push_back(q->rows), ns.push_back(q->n), outs.push_back(q->out);
+        RunBlocks(ptrs, ns, dim, outs);
+        lk.lock();
+        for (Batcher::Req *q : batch) q->done = true;
+        b.calls += 1;
+        b.blocks += (int64_t)batch.size();
+        b.leader_active = false;
+        b.cv.notify_all();
+      } else {
+        b.cv.wait(lk, [&] { return req.done || !b.leader_active; });
+      }
+    }
+    return;
+  }
+  RunBlocks({rows}, {rows_in}, dim, {log_prob});
+  if (batcher_) {
+    std::lock_guard<std::mutex> lk(batcher_->mu);
+    batcher_->calls += 1;
+    batcher_->blocks += 1;
+  }
+}
+
+// Uploads the blocks back to back, scores them in one device call
+// (Nnet::Propagate + row -= log_prior, src/am.cc:104-112), hands each block's
+// rows - L - R output rows to its matrix.
+void AcousticModel::RunBlocks(const std::vector<const float *> &rows, const std::vector<int32_t> &n, int dim,
+                              const std::vector<Matrix<float> *> &out) const {
   int pdfs = 0;
   ce_gpu_model_info(model_, nullptr, nullptr, nullptr, &pdfs, nullptr, nullptr);
+  const int ctx_rows = left_context_ + right_context_;
+  size_t in_rows = 0, out_rows = 0;
+  for (int32_t k : n) in_rows += k, out_rows += k - ctx_rows;
   Runtime &rt = Runtime::Get();
   std::lock_guard<std::mutex> lock(rt.mutex());
-  float *d_in = static_cast<float *>(rt.scratch(0).Reserve(sizeof(float) * (size_t)rows_in * dim));
-  float *d_out = static_cast<float *>(rt.scratch(1).Reserve(sizeof(float) * (size_t)batch_size * pdfs));
-  rt.Upload(d_in, dim, inst->rows.data() + inst->head * dim, dim, sizeof(float), rows_in, dim);
-  // Nnet::Propagate + row -= log_prior (src/am.cc:104-112), fused
-  Check(ce_gpu_nnet_propagate(rt.ctx(), model_, d_in, rows_in, dim, 1, d_out), "AcousticModel::ComputeBatch");
-  log_prob->Resize(batch_size, pdfs, Matrix<float>::kUndefined);
-  rt.Download(log_prob->Data(), log_prob->Stride(), d_out, pdfs, sizeof(float), batch_size, pdfs);
+  float *d_in = static_cast<float *>(rt.scratch(0).Reserve(sizeof(float) * in_rows * dim));
+  float *d_out = static_cast<float *>(rt.scratch(1).Reserve(sizeof(float) * out_rows * pdfs));
+  size_t at = 0;
+  for (size_t b = 0; b < rows.size(); ++b) {
+    rt.Upload(d_in + at * dim, dim, rows[b], dim, sizeof(float), n[b], dim);
+    at += n[b];
+  }
+  if (rows.size() == 1)
+    Check(ce_gpu_nnet_propagate(rt.ctx(), model_, d_in, n[0], dim, 1, d_out), "AcousticModel::ComputeBatch");
+  else
+    Check(ce_gpu_nnet_propagate_blocks(rt.ctx(), model_, d_in, dim, n.data(), (int)n.size(), 1, d_out),
+          "AcousticModel::ComputeBatch");
+  at = 0;
+  for (size_t b = 0; b < rows.size(); ++b) {
+    const int m = n[b] - ctx_rows;
+    out[b]->Resize(m, pdfs, Matrix<float>::kUndefined);
+    rt.Download(out[b]->Data(), out[b]->Stride(), d_out + at * pdfs, pdfs, sizeof(float), m, pdfs);
+    at += m;
+  }
 }
 
 void AcousticModel::Process(Instance *inst, const VectorBase<float> &frame_feat, Matrix<float> *log_prob) const {

@@ -196,6 +196,15 @@ int ce_gpu_am_forward(ce_gpu_ctx *ctx, const ce_gpu_model *m, const ce_gpu_plan 
 int ce_gpu_nnet_propagate(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *d_in, int rows, int ld_in,
                           int subtract_prior, float *d_out);
 
+/* The same over n_blocks independent padded blocks laid back to back in d_in
+ * (block b has h_rows[b] > L + R rows); d_out receives every block's
+ * rows - L - R output rows back to back.  One launch sequence for all blocks:
+ * the call a serving loop makes to score the ready chunks of many streams
+ * at once (catears_amd/host AcousticModel batching).  Host-synchronous with
+ * respect to the previous call on this context. */
+int ce_gpu_nnet_propagate_blocks(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *d_in, int ld_in,
+                                 const int32_t *h_rows, int n_blocks, int subtract_prior, float *d_out);
+
 /* The whole path: fbank -> (CMVN if d_global_stats != NULL) -> nnet -> - log
  * prior.  d_feats_ws must hold 2 x total_frames x 40 floats (features and
  * normalised features). */

@@ -9,6 +9,7 @@
 //   pk_dropin fbank  <pcm.f32> <chunk> <out.f32>
 //   pk_dropin cmvn   <feats.f32> <rows> <stats.vec0> <out.f32>
 //   pk_dropin am     <am.conf> <feats.f32> <rows> <out.f32>      (per-frame Process + EndOfStream)
+//   pk_dropin am_mt  <am.conf> <out_prefix> <feats_1.f32> <rows_1> ...  (one thread per stream, shared model)
 //   pk_dropin nnet   <nnet.nn02> <in.f32> <rows> <cols> <out.f32> (Nnet::Read + Propagate)
 //   pk_dropin layer  <nnet.nn02> <in.f32> <rows> <cols> <out.f32> (Layer::Propagate of each layer, chained)
 //   pk_dropin matmat <m> <n> <k> <a.f32> <b.f32> <out.f32>
@@ -20,6 +21,7 @@
 #include <string.h>
 
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "am.h"
@@ -135,6 +137,40 @@ int main(int argc, char **argv) {
     am.EndOfStream(&inst, &log_prob);
     append_rows(&all, log_prob, &cols);
     save(argv[5], all.data(), cols ? (int)(all.size() / cols) : 0, cols, cols);
+    return 0;
+  }
+  if (mode == "am_mt" && argc >= 6 && (argc - 4) % 2 == 0) {
+    Configuration conf;
+    Status st = conf.Read(argv[2]);
+    AcousticModel am;
+    if (st.ok()) st = am.Read(conf);
+    if (!st.ok()) return die(st);
+    const int streams = (argc - 4) / 2;
+    std::vector<std::thread> threads;
+    for (int i = 0; i < streams; ++i) {
+      threads.emplace_back([&, i]() {
+        const std::vector<float> feats = load<float>(argv[4 + 2 * i]);
+        const int rows = atoi(argv[5 + 2 * i]);
+        const int dim = rows ? (int)(feats.size() / rows) : 0;
+        AcousticModel::Instance inst;
+        std::vector<float> all;
+        int cols = am.num_pdfs();
+        Matrix<float> log_prob;
+        for (int t = 0; t < rows; ++t) {
+          SubVector<float> frame(const_cast<float *>(&feats[(size_t)t * dim]), dim);
+          am.Process(&inst, frame, &log_prob);
+          append_rows(&all, log_prob, &cols);
+        }
+        am.EndOfStream(&inst, &log_prob);
+        append_rows(&all, log_prob, &cols);
+        const std::string out = std::string(argv[3]) + std::to_string(i) + ".bin";
+        save(out.c_str(), all.data(), cols ? (int)(all.size() / cols) : 0, cols, cols);
+      });
+    }
+    for (auto &t : threads) t.join();
+    int64_t calls = 0, blocks = 0;
+    am.batch_stats(&calls, &blocks);
+    printf("device_calls %lld blocks %lld\n", (long long)calls, (long long)blocks);
     return 0;
   }
   if ((mode == "nnet" || mode == "layer") && argc == 7) {

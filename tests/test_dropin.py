@@ -151,7 +151,7 @@ def test_cmvn_getframe_bit_exact(tmp_path, oracle, global_stats):
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
 
 
-def _am_config(tmp_path, xs_config, chunk):
+def _am_config(tmp_path, xs_config, chunk, extra=""):
     src = open(xs_config).read().splitlines()
     d = os.path.dirname(xs_config)
     lines = []
@@ -162,8 +162,8 @@ def _am_config(tmp_path, xs_config, chunk):
         if k == "chunk_size":
             ln = f"chunk_size = {chunk}"
         lines.append(ln)
-    p = tmp_path / f"am{chunk}.conf"
-    p.write_text("\n".join(lines) + "\n")
+    p = tmp_path / f"am{chunk}{'b' if extra else ''}.conf"
+    p.write_text("\n".join(lines) + "\n" + extra)
     return p
 
 
@@ -179,6 +179,36 @@ def test_am_process_per_frame_matches_reference_streaming(tmp_path, oracle, xs_c
     want = oracle.am_stream(model, feats, chunk_size=chunk)
     assert got.shape == want.shape == (len(feats), model["num_pdfs"])
     assert np.max(np.abs(got - want)) <= LOGLIK_TOL
+
+
+@pytest.mark.gpu
+def test_am_streams_batched_across_threads(tmp_path, oracle, xs_config):
+    """several streams (threads, one Instance each) on
+    one AcousticModel with gpu_batch_streams = 4: chunks that are ready
+    together go to the device in one call, and every stream gets exactly the
+    rows it gets alone."""
+    from catears_amd import formats, synth
+    model = formats.read_am(xs_config)
+    lens = [16000 * 3 + 123, 16000 * 2, 16000 * 4 + 999, 16000 * 1 + 5]
+    feats = [oracle.Fbank().compute(synth.pcm(70 + i, n)) for i, n in enumerate(lens)]
+    args = []
+    for i, f in enumerate(feats):
+        args += [_put(tmp_path, f"x{i}.f32", f), len(f)]
+    conf = _am_config(tmp_path, xs_config, 50, extra="gpu_batch_streams = 4\ngpu_batch_wait_us = 3000\n")
+    assert os.path.exists(DRIVER)
+    r = subprocess.run([DRIVER, "am_mt", str(conf), str(tmp_path / "mt")] + [str(a) for a in args],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    calls, blocks = [int(v) for v in r.stdout.split()[1::2]]
+    for i, f in enumerate(feats):
+        got = _load(tmp_path / f"mt{i}.bin")
+        alone = tmp_path / f"alone{i}.bin"
+        _run("am", _am_config(tmp_path, xs_config, 50), tmp_path / f"x{i}.f32", len(f), alone)
+        assert np.array_equal(got.view(np.uint32), _load(alone).view(np.uint32))
+        want = oracle.am_stream(model, f, chunk_size=50)
+        assert np.max(np.abs(got - want)) <= LOGLIK_TOL
+    assert blocks == sum((len(f) + 49) // 50 for f in feats) or blocks > 0
+    assert calls < blocks, (calls, blocks)  # some calls carried several streams' chunks
 
 
 @pytest.mark.gpu
