@@ -41,7 +41,7 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(PKLIB) $(PKTEST)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean

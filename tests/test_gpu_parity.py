@@ -87,6 +87,31 @@ def test_fbank_ragged_batch_edges(torch, G, ctx, oracle):
             assert np.abs(f[off[u]:off[u + 1]] - of).max() <= FEAT_TOL
 
 
+def test_fbank_full_c2_scale(torch, G, ctx, oracle):
+    """BASELINE config C2 at full size -- 1000 x 10 s utterances, 998 000
+    frames in one launch -- every pre-log mel energy bit-exact against the
+    oracle, plus the size-independent property that an utterance's frames do
+    not depend on its neighbours (the batch reversed gives the same rows)."""
+    from catears_amd import synth
+    n = 160000
+    base = [synth.pcm(5000 + i, n) for i in range(40)]
+    waves = [base[i % 40] * (1.0 if (i // 40) % 2 == 0 else -1.0) for i in range(1000)]  # 80 distinct
+    plan, off, f, m = gpu_fbank(torch, G, ctx, waves)
+    assert plan.total_frames == 998000
+    fb = oracle.Fbank()
+    ref = {}
+    for i in range(80):
+        ref[i] = fb.compute(waves[i], with_mel=True)
+    for u in range(1000):
+        of, om = ref[u % 80]
+        assert np.array_equal(bits(m[off[u]:off[u + 1]]), bits(om)), f"utt {u}"
+        assert np.abs(f[off[u]:off[u + 1]] - of).max() <= FEAT_TOL
+    plan_r, off_r, f_r, m_r = gpu_fbank(torch, G, ctx, waves[::-1])
+    for u in range(0, 1000, 37):
+        v = 999 - u
+        assert np.array_equal(bits(m[off[u]:off[u + 1]]), bits(m_r[off_r[v]:off_r[v + 1]]))
+
+
 # ------------------------------------------------------------------- cmvn --
 
 def test_cmvn_bitexact(torch, G, ctx, oracle, global_stats):
