@@ -34,76 +34,74 @@ CE_HD float preemph(float cur, float prev) {
 // Pure placement: values and arithmetic are unchanged.
 CE_HD int sw(int i) { return i ^ ((i >> 2) & 63); }
 
-// One lane op of the split-radix generation schedule (src/srfft.cc:124-265).
-// op = kind(2) | lg(4) | n(8) | base(8); see tables.cc build_fft_schedule.
-CE_HD void fft_lane_op(uint32_t op, float *re, float *im, const float *twiddle,
-                       const int *twiddle_base) {
-  const uint32_t kind = op & 3u;
+// One lane op of the split-radix generation schedule (src/srfft.cc:124-265),
+// from its precomputed descriptor (tables.cc build_fft_lanes):
+//   addr  the op's four LDS slots, already swizzled, 8 bits each (slot j in
+//         bits 8j..8j+7): points base+n, +q, +h, +h+q of a node of length
+//         m = 2^lg (q = m/4, h = m/2); base..base+3 of a length-4 node;
+//         base, base+1 of a length-2 node
+//   meta  kind (bits 0-1: 0 none, 1 node, 2 length-4, 3 length-2) | twiddle
+//         case (bits 2-3: 0 none (n == 0), 1 the n == m/8 rotation, 2 table)
+//   tw    the node's six table twiddles for this n (table case)
+CE_HD void fft_lane_op(uint32_t addr, uint32_t meta, const float *tw, float *re, float *im) {
+  const uint32_t kind = meta & 3u;
   if (kind == 0u) return;
-  const int lg = (int)((op >> 2) & 15u), n = (int)((op >> 6) & 255u), base = (int)(op >> 14);
+  const int p0 = (int)(addr & 255u), p1 = (int)((addr >> 8) & 255u);
+  const int p2 = (int)((addr >> 16) & 255u), p3 = (int)(addr >> 24);
   float t1, t2;
   if (kind == 3u) {  // length-2 node (srfft.cc:206-216)
-    const int s0 = sw(base), s1 = sw(base + 1);
-    t1 = re[s0] + re[s1]; re[s1] = re[s0] - re[s1]; re[s0] = t1;
-    t1 = im[s0] + im[s1]; im[s1] = im[s0] - im[s1]; im[s0] = t1;
+    t1 = re[p0] + re[p1]; re[p1] = re[p0] - re[p1]; re[p0] = t1;
+    t1 = im[p0] + im[p1]; im[p1] = im[p0] - im[p1]; im[p0] = t1;
     return;
   }
-  if (kind == 2u) {  // length-4 node (srfft.cc:163-205)
-    const int s0 = sw(base), s1 = sw(base + 1), s2 = sw(base + 2), s3 = sw(base + 3);
-    float r[4] = {re[s0], re[s1], re[s2], re[s3]}, i[4] = {im[s0], im[s1], im[s2], im[s3]};
-    t1 = r[0] + r[2]; r[2] = r[0] - r[2]; r[0] = t1;
-    t1 = i[0] + i[2]; i[2] = i[0] - i[2]; i[0] = t1;
-    t1 = r[1] + r[3]; r[3] = r[1] - r[3]; r[1] = t1;
-    t1 = i[1] + i[3]; i[3] = i[1] - i[3]; i[1] = t1;
-    t1 = r[0] + r[1]; r[1] = r[0] - r[1]; r[0] = t1;
-    t1 = i[0] + i[1]; i[1] = i[0] - i[1]; i[0] = t1;
-    t1 = r[2] + i[3];
-    t2 = i[2] + r[3];
-    i[2] = i[2] - r[3];
-    r[3] = r[2] - i[3];
-    r[2] = t1;
-    i[3] = t2;
-    re[s0] = r[0]; re[s1] = r[1]; re[s2] = r[2]; re[s3] = r[3];
-    im[s0] = i[0]; im[s1] = i[1]; im[s2] = i[2]; im[s3] = i[3];
-    return;
-  }
-  // general node of length m = 2^lg: this lane owns n, n+q, n+h, n+h+q
-  const int q = 1 << (lg - 2), h = 2 * q, e = q / 2;
-  const int p0 = sw(base + n), p1 = sw(base + n + q), p2 = sw(base + n + h), p3 = sw(base + n + h + q);
   float ar = re[p0], ai = im[p0], br = re[p1], bi = im[p1];
   float cr = re[p2], ci = im[p2], dr = re[p3], di = im[p3];
-  // step 1: butterflies (n, n+h) and (n+q, n+q+h)
-  t1 = ar + cr; cr = ar - cr; ar = t1;
-  t1 = ai + ci; ci = ai - ci; ai = t1;
-  t1 = br + dr; dr = br - dr; br = t1;
-  t1 = bi + di; di = bi - di; bi = t1;
-  // step 2: (h+n, h+q+n)
-  t1 = cr + di;
-  t2 = ci + dr;
-  ci = ci - dr;
-  dr = cr - di;
-  cr = t1;
-  di = t2;
-  // steps 3 & 4: twiddles for n >= 1
-  if (n == e) {
-    const float sq = (float)0.70710678118654752440;
-    t1 = sq * (cr + ci);
-    ci = sq * (ci - cr);
+  if (kind == 2u) {  // length-4 node (srfft.cc:163-205), points a b c d = 0 1 2 3
+    t1 = ar + cr; cr = ar - cr; ar = t1;
+    t1 = ai + ci; ci = ai - ci; ai = t1;
+    t1 = br + dr; dr = br - dr; br = t1;
+    t1 = bi + di; di = bi - di; bi = t1;
+    t1 = ar + br; br = ar - br; ar = t1;
+    t1 = ai + bi; bi = ai - bi; ai = t1;
+    t1 = cr + di;
+    t2 = ci + dr;
+    ci = ci - dr;
+    dr = cr - di;
     cr = t1;
-    t2 = sq * (di - dr);
-    di = -sq * (dr + di);
-    dr = t2;
-  } else if (n > 0) {
-    const int nel = q - 2, w = n - 1 - (n > e ? 1 : 0);
-    const float *tw = twiddle + twiddle_base[lg];
-    t2 = tw[w] * (cr + ci);
-    t1 = tw[nel + w] * cr + t2;
-    cr = tw[2 * nel + w] * ci + t2;
-    ci = t1;
-    t2 = tw[3 * nel + w] * (dr + di);
-    t1 = tw[4 * nel + w] * dr + t2;
-    dr = tw[5 * nel + w] * di + t2;
-    di = t1;
+    di = t2;
+  } else {  // general node: this lane owns n, n+q, n+h, n+h+q
+    // step 1: butterflies (n, n+h) and (n+q, n+q+h)
+    t1 = ar + cr; cr = ar - cr; ar = t1;
+    t1 = ai + ci; ci = ai - ci; ai = t1;
+    t1 = br + dr; dr = br - dr; br = t1;
+    t1 = bi + di; di = bi - di; bi = t1;
+    // step 2: (h+n, h+q+n)
+    t1 = cr + di;
+    t2 = ci + dr;
+    ci = ci - dr;
+    dr = cr - di;
+    cr = t1;
+    di = t2;
+    // steps 3 & 4: twiddles for n >= 1
+    const uint32_t twc = (meta >> 2) & 3u;
+    if (twc == 1u) {
+      const float sq = (float)0.70710678118654752440;
+      t1 = sq * (cr + ci);
+      ci = sq * (ci - cr);
+      cr = t1;
+      t2 = sq * (di - dr);
+      di = -sq * (dr + di);
+      dr = t2;
+    } else if (twc == 2u) {
+      t2 = tw[0] * (cr + ci);
+      t1 = tw[1] * cr + t2;
+      cr = tw[2] * ci + t2;
+      ci = t1;
+      t2 = tw[3] * (dr + di);
+      t1 = tw[4] * dr + t2;
+      dr = tw[5] * di + t2;
+      di = t1;
+    }
   }
   re[p0] = ar; im[p0] = ai; re[p1] = br; im[p1] = bi;
   re[p2] = cr; im[p2] = ci; re[p3] = dr; im[p3] = di;

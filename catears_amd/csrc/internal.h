@@ -74,6 +74,10 @@ struct FbankTables {
   int twiddle_base[9];              // start of level lg in `twiddle`
   float kn[2 * 129];                // real-FFT post twiddles kN_k, k = 1..128
   uint32_t fft_ops[kFftGens * 64];  // per generation, per lane node op
+  // the same ops as the lane descriptors fb::fft_lane_op executes
+  uint32_t fft_addr[kFftGens * 64];  // four swizzled LDS slots, 8 bits each
+  uint32_t fft_meta[kFftGens * 64];  // kind | twiddle case << 2
+  float fft_tw[kFftGens * 64 * 6];   // the op's six table twiddles
   int mel_off[kMel];                // first FFT bin of each triangle
   int mel_len[kMel];
   int mel_wbase[kMel];              // start of its weights in mel_w

@@ -34,7 +34,7 @@ constexpr int kFramesPerBlock = 4;  // one wave per frame, 4 waves per block
 #ifndef FBANK_GENS
 #define FBANK_GENS kFftGens  // (timing experiments only may lower it)
 #endif
-constexpr int kBlocksPerCU = 6;     // residency of fbank_kernel (26 KB LDS, 78 VGPRs)
+constexpr int kBlocksPerCU = 5;     // residency of fbank_kernel (31 KB LDS, 82 VGPRs)
 constexpr int kMaxBlocks = 256 * kBlocksPerCU;
 
 __device__ __forceinline__ void wave_sync() {
@@ -55,12 +55,13 @@ struct WaveSmem {
   float im[kHalf];
 };
 
-// Tables staged once per block in LDS (indexed by op / band at run time).
+// Tables staged once per block in LDS (indexed by generation / band at run
+// time): each lane op's descriptor (slots, kind, twiddles) and mel weights.
 struct BlockTables {
-  float twiddle[6 * 64 * 5];
+  float tw[kFftGens * 64 * 6];  // each lane op's six twiddles
+  uint32_t addr[kFftGens * 64];
+  uint32_t meta[kFftGens * 64];
   float mel_w[512];
-  uint32_t ops[kFftGens * 64];
-  int twiddle_base[9];
 };
 
 // Persistent blocks: each block stages the frame-independent tables once --
@@ -79,10 +80,9 @@ __global__ __launch_bounds__(256) void fbank_kernel(const FbankTables *__restric
   __shared__ WaveSmem smem[kFramesPerBlock];
   __shared__ BlockTables bt;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int i = threadIdx.x; i < 6 * 64 * 5; i += 256) bt.twiddle[i] = tab->twiddle[i];
+  for (int i = threadIdx.x; i < kFftGens * 64 * 6; i += 256) bt.tw[i] = tab->fft_tw[i];
+  for (int i = threadIdx.x; i < kFftGens * 64; i += 256) bt.addr[i] = tab->fft_addr[i], bt.meta[i] = tab->fft_meta[i];
   for (int i = threadIdx.x; i < 512; i += 256) bt.mel_w[i] = tab->mel_w[i];
-  for (int i = threadIdx.x; i < kFftGens * 64; i += 256) bt.ops[i] = tab->fft_ops[i];
-  if (threadIdx.x < 9) bt.twiddle_base[threadIdx.x] = tab->twiddle_base[threadIdx.x];
   float win[7];
 #pragma unroll
   for (int j = 0; j < 7; ++j) {
@@ -146,7 +146,8 @@ __global__ __launch_bounds__(256) void fbank_kernel(const FbankTables *__restric
     // 3. split-radix generations
 #pragma unroll 1
     for (int g = 0; g < FBANK_GENS; ++g) {
-      fb::fft_lane_op(bt.ops[g * 64 + lane], S.re, S.im, bt.twiddle, bt.twiddle_base);
+      const int o = g * 64 + lane;
+      fb::fft_lane_op(bt.addr[o], bt.meta[o], bt.tw + 6 * o, S.re, S.im);
       wave_sync();
     }
 

@@ -17,6 +17,7 @@
 
 #include <vector>
 
+#include "fbank_ops.h"
 #include "internal.h"
 
 namespace catears {
@@ -147,6 +148,38 @@ void build_fft_schedule(FbankTables *t) {
       t->fft_ops[g * 64 + l] = l < (int)gens[g].size() ? gens[g][l] : fft_op(kOpNone, 0, 0, 0);
 }
 
+// Lane descriptors of the scheduled ops (fbank_ops.h fft_lane_op): the LDS
+// slots and twiddle values each op touches, resolved on the host so the
+// kernel's lanes do no index arithmetic.
+void build_fft_lanes(FbankTables *t) {
+  for (int i = 0; i < kFftGens * 64; ++i) {
+    const uint32_t op = t->fft_ops[i];
+    const uint32_t kind = op & 3u;
+    const int lg = (int)((op >> 2) & 15u), n = (int)((op >> 6) & 255u), base = (int)(op >> 14);
+    int pts[4] = {0, 0, 0, 0};
+    uint32_t twc = 0;
+    if (kind == kOpLeaf2) {
+      pts[0] = base, pts[1] = base + 1, pts[2] = base, pts[3] = base + 1;
+    } else if (kind == kOpLeaf4) {
+      for (int j = 0; j < 4; ++j) pts[j] = base + j;
+    } else if (kind == kOpNode) {
+      const int q = 1 << (lg - 2), h = 2 * q, e = q / 2;
+      pts[0] = base + n, pts[1] = base + n + q, pts[2] = base + n + h, pts[3] = base + n + h + q;
+      if (n == e) {
+        twc = 1;
+      } else if (n > 0) {
+        twc = 2;
+        const int nel = q - 2, w = n - 1 - (n > e ? 1 : 0);
+        for (int j = 0; j < 6; ++j) t->fft_tw[i * 6 + j] = t->twiddle[t->twiddle_base[lg] + j * nel + w];
+      }
+    }
+    uint32_t addr = 0;
+    for (int j = 0; j < 4; ++j) addr |= (uint32_t)fb::sw(pts[j]) << (8 * j);
+    t->fft_addr[i] = addr;
+    t->fft_meta[i] = kind | (twc << 2);
+  }
+}
+
 }  // namespace
 
 void build_fbank_tables(FbankTables *t) {
@@ -156,6 +189,7 @@ void build_fbank_tables(FbankTables *t) {
   build_twiddles(t);
   build_post_twiddles(t);
   build_fft_schedule(t);
+  build_fft_lanes(t);
 }
 
 }  // namespace catears

@@ -48,7 +48,10 @@ extern "C" int emu_fbank(const float *wave, long n, float *mel, float *feats) {
     }
     for (int i = kWinLen / 2; i < kHalf; ++i) re[fb::sw(i)] = im[fb::sw(i)] = 0.0f;
     for (int g = 0; g < kFftGens; ++g)
-      for (int l = 0; l < 64; ++l) fb::fft_lane_op(tab.fft_ops[g * 64 + l], re, im, tab.twiddle, tab.twiddle_base);
+      for (int l = 0; l < 64; ++l) {
+        const int o = g * 64 + l;
+        fb::fft_lane_op(tab.fft_addr[o], tab.fft_meta[o], tab.fft_tw + 6 * o, re, im);
+      }
     for (int l = 0; l < 64; ++l) {
       fb::post_power(l + 1, re, im, tab.kn, pw);
       fb::post_power(l + 65, re, im, tab.kn, pw);
