@@ -66,6 +66,47 @@ __global__ __launch_bounds__(256) void finalize_kernel(const float *__restrict__
   }
 }
 
+// The same with 16-byte accesses (dim, ldx multiples of 4, aligned rows):
+// lane l holds float4 chunks l, l + 64, ... of its row.
+constexpr int kMaxVecPerLane = 16;  // rows up to 4096 wide
+
+template <bool LOGSM>
+__global__ __launch_bounds__(256) void finalize_vec_kernel(const float *__restrict__ x, int ldx, int rows, int dim,
+                                                           const float *__restrict__ prior,
+                                                           const int *__restrict__ row_dst,
+                                                           float *__restrict__ out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int dst = row_dst ? row_dst[row] : row;
+  if (dst < 0) return;
+  const float4 *xr = reinterpret_cast<const float4 *>(x + (int64_t)row * ldx);
+  float4 *o = reinterpret_cast<float4 *>(out + (int64_t)dst * dim);
+  const float4 *pr = reinterpret_cast<const float4 *>(prior);
+  const int d4 = dim >> 2;
+  float4 v[kMaxVecPerLane];
+  float s = 0.0f;
+#pragma unroll
+  for (int j = 0; j < kMaxVecPerLane; ++j) {
+    const int c = lane + 64 * j;
+    v[j] = c < d4 ? xr[c] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (LOGSM && c < d4) s += expf(v[j].x) + expf(v[j].y) + expf(v[j].z) + expf(v[j].w);
+  }
+  const float ls = LOGSM ? logf(wave_sum(s)) : 0.0f;
+#pragma unroll
+  for (int j = 0; j < kMaxVecPerLane; ++j) {
+    const int c = lane + 64 * j;
+    if (c < d4) {
+      float4 y = v[j];
+      if (LOGSM) y = make_float4(y.x - ls, y.y - ls, y.z - ls, y.w - ls);
+      if (prior) {
+        const float4 p = pr[c];
+        y = make_float4(y.x - p.x, y.y - p.y, y.z - p.z, y.w - p.w);
+      }
+      o[c] = y;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void rowop_kernel(int kind, float *__restrict__ x, int ldx, int rows,
                                                     int dim, const float *__restrict__ scale,
                                                     const float *__restrict__ offset) {
@@ -173,6 +214,17 @@ int launch_finalize(hipStream_t s, const float *x, int ldx, int rows, int dim, b
                     const float *log_prior, const int *row_dst, float *out) {
   if (rows <= 0) return CE_GPU_OK;
   dim3 grid((rows + 3) / 4), block(256);
+  const bool vec = dim % 4 == 0 && ldx % 4 == 0 && dim <= 4 * 64 * kMaxVecPerLane &&
+                   ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out) |
+                     reinterpret_cast<uintptr_t>(log_prior)) & 15) == 0;
+  if (vec) {
+    if (log_softmax)
+      hipLaunchKernelGGL(finalize_vec_kernel<true>, grid, block, 0, s, x, ldx, rows, dim, log_prior, row_dst, out);
+    else
+      hipLaunchKernelGGL(finalize_vec_kernel<false>, grid, block, 0, s, x, ldx, rows, dim, log_prior, row_dst, out);
+    CE_HIP(hipGetLastError());
+    return CE_GPU_OK;
+  }
   if (log_softmax)
     hipLaunchKernelGGL(finalize_kernel<true>, grid, block, 0, s, x, ldx, rows, dim, log_prior,
                        row_dst, out);
