@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "catears_gpu.h"
@@ -98,6 +99,55 @@ inline uint32_t fft_op(uint32_t kind, uint32_t lg, uint32_t n, uint32_t base) {
 
 // Post-ops fused into a GEMM epilogue (applied in order, up to 4).
 enum PostOp : int { kPostNone = 0, kPostRelu = 1, kPostBatchNorm = 2 };
+
+// The chains nnet programs produce, as one uniform mode per launch so an
+// epilogue is straight-line code (a runtime loop over the chain per element
+// is a scalar branch ladder per stored value).  kPostModeGeneric keeps the
+// loop for anything else.
+enum PostMode : int {
+  kPostModeNone = 0, kPostModeRelu = 1, kPostModeBn = 2, kPostModeReluBn = 3, kPostModeBnRelu = 4,
+  kPostModeGeneric = 5
+};
+inline int post_mode(const int *post, int npost) {
+  if (npost == 0) return kPostModeNone;
+  if (npost == 1) return post[0] == kPostRelu ? kPostModeRelu : post[0] == kPostBatchNorm ? kPostModeBn : kPostModeGeneric;
+  if (npost == 2 && post[0] == kPostRelu && post[1] == kPostBatchNorm) return kPostModeReluBn;
+  if (npost == 2 && post[0] == kPostBatchNorm && post[1] == kPostRelu) return kPostModeBnRelu;
+  return kPostModeGeneric;
+}
+
+// y after the post chain in the reference's rounding order (ReLU as
+// y < 0 ? 0 : y, which keeps NaN; BatchNorm as a rounded product then a
+// rounded sum, matrix.cc / nnet.cc).
+template <int MODE>
+__device__ __forceinline__ float apply_post(float y, float sc, float of, const int *post, int npost) {
+  auto relu = [](float v) { return v < 0.0f ? 0.0f : v; };
+  auto bn = [&](float v) {
+    v = v * sc;
+    return v + of;
+  };
+  if (MODE == kPostModeRelu) return relu(y);
+  if (MODE == kPostModeBn) return bn(y);
+  if (MODE == kPostModeReluBn) return bn(relu(y));
+  if (MODE == kPostModeBnRelu) return relu(bn(y));
+  if (MODE == kPostModeGeneric) {
+    for (int q = 0; q < npost; ++q) y = post[q] == kPostRelu ? relu(y) : post[q] == kPostBatchNorm ? bn(y) : y;
+  }
+  return y;
+}
+
+// Calls f(std::integral_constant<int, MODE>) for the runtime mode.
+template <class F>
+__device__ __forceinline__ void with_post_mode(int mode, F &&f) {
+  switch (mode) {
+    case kPostModeNone: f(std::integral_constant<int, kPostModeNone>()); break;
+    case kPostModeRelu: f(std::integral_constant<int, kPostModeRelu>()); break;
+    case kPostModeBn: f(std::integral_constant<int, kPostModeBn>()); break;
+    case kPostModeReluBn: f(std::integral_constant<int, kPostModeReluBn>()); break;
+    case kPostModeBnRelu: f(std::integral_constant<int, kPostModeBnRelu>()); break;
+    default: f(std::integral_constant<int, kPostModeGeneric>()); break;
+  }
+}
 
 struct GemmLayer {
   int din = 0;            // input row width (one splice segment)

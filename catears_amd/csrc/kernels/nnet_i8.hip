@@ -209,11 +209,67 @@ struct I8Args {
   int32_t w_zp;
   const float *bias, *bn_scale, *bn_offset;
   int post[4];
-  int npost;
+  int npost, post_mode;
   float *y;
   int ldy;
   int tiles_n, tiles_m, group;
 };
+
+// Zero-point restore + bias + ReLU / BatchNorm + store of one wave's
+// (TI x 32) x (TJ x 32) accumulator tile at (m0 + wrow, col0).  Column
+// constants are read once into registers (the output stores could alias them
+// as far as the compiler knows, so reads inside the store loop reload after
+// every store) and the spliced row sums once per block row into LDS (`srs`,
+// BM words; a per-lane loop over rows x segments is a chain of dependent L2
+// round trips).  Every thread of the block must call it.
+template <int TI, int TJ, int BM, int NT>
+__device__ __forceinline__ void i8_epilogue(const I8Args &p, const i32x16 (&acc)[TI][TJ], int m0, int wrow, int col0,
+                                            int r, int h, uint32_t *srs) {
+  const QP pa = *static_cast<const QP *>(p.pa);
+  const uint32_t ca = (uint32_t)(128 - pa.zp), cb = (uint32_t)(128 - p.w_zp);
+  const uint32_t kterm = (uint32_t)p.k * ca * cb;
+  const float cscale = pa.scale * p.w_scale;  // matrix.cc:404-405
+  // cB * row sum of each spliced row of the block, one row per thread, into
+  // LDS (the operand buffers are free once every wave is past the loop)
+  __syncthreads();
+  for (int t = threadIdx.x; t < BM; t += NT) {
+    const int row = m0 + t;
+    uint32_t sum = 0;
+#pragma unroll
+    for (int sg = 0; sg < 8; ++sg) {
+      if (sg < p.nseg) {
+        int src = row + p.off[sg];
+        src = src < 0 ? 0 : (src > p.m - 1 ? p.m - 1 : src);
+        sum += (uint32_t)p.rowsum[src];
+      }
+    }
+    srs[t] = cb * sum;
+  }
+  __syncthreads();
+  with_post_mode(p.post_mode, [&](auto M) {
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int col = col0 + j * 32 + r;
+      if (col >= p.n) continue;
+      const uint32_t cterm = ca * (uint32_t)p.colsum[col] + kterm;
+      const float bias = p.bias ? p.bias[col] : 0.0f;
+      const float sc = p.bn_scale ? p.bn_scale[col] : 1.0f;
+      const float of = p.bn_offset ? p.bn_offset[col] : 0.0f;
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int lr = wrow + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+          const uint32_t v = (uint32_t)acc[i][j][e] + srs[lr] + cterm;
+          float y = (float)(int32_t)v * cscale;
+          y = y + bias;  // +0 when absent: y is never -0 here (int * positive scale)
+          y = apply_post<decltype(M)::value>(y, sc, of, p.post, p.npost);
+          if (m0 + lr < p.m) p.y[(int64_t)(m0 + lr) * p.ldy + col] = y;
+        }
+      }
+    }
+  });
+}
 
 __global__ __launch_bounds__(256, 2) void gemm_i8_nnet_kernel(I8Args p) {
   __shared__ __attribute__((aligned(16))) int8_t As[IBM * ILD];
@@ -271,41 +327,7 @@ __global__ __launch_bounds__(256, 2) void gemm_i8_nnet_kernel(I8Args p) {
     __syncthreads();
   }
 
-  const QP pa = *static_cast<const QP *>(p.pa);
-  const uint32_t ca = (uint32_t)(128 - pa.zp), cb = (uint32_t)(128 - p.w_zp);
-  const uint32_t kterm = (uint32_t)p.k * ca * cb;
-  const float cscale = pa.scale * p.w_scale;  // matrix.cc:404-405
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int row = m0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-      if (row >= p.m) continue;
-      uint32_t rs = 0;  // row sum of the spliced row
-      for (int sg = 0; sg < p.nseg; ++sg) {
-        int src = row + p.off[sg];
-        src = src < 0 ? 0 : (src > p.m - 1 ? p.m - 1 : src);
-        rs += (uint32_t)p.rowsum[src];
-      }
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int col = n0 + wn * 64 + j * 32 + r;
-        if (col >= p.n) continue;
-        const uint32_t v = (uint32_t)acc[i][j][e] + cb * rs + ca * (uint32_t)p.colsum[col] + kterm;
-        float y = (float)(int32_t)v * cscale;
-        if (p.bias) y = y + p.bias[col];
-        for (int q = 0; q < p.npost; ++q) {
-          if (p.post[q] == kPostRelu) {
-            y = y < 0.0f ? 0.0f : y;
-          } else if (p.post[q] == kPostBatchNorm) {
-            y = y * p.bn_scale[col];
-            y = y + p.bn_offset[col];
-          }
-        }
-        p.y[(int64_t)row * p.ldy + col] = y;
-      }
-    }
-  }
+  i8_epilogue<2, 2, IBM, 256>(p, acc, m0, wm * 64, n0 + wn * 64, r, h, reinterpret_cast<uint32_t *>(As));
 }
 
 
@@ -414,41 +436,118 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_i8_glds_kernel(I8Args 
     }
   }
 
-  const QP pa = *static_cast<const QP *>(p.pa);
-  const uint32_t ca = (uint32_t)(128 - pa.zp), cb = (uint32_t)(128 - p.w_zp);
-  const uint32_t kterm = (uint32_t)p.k * ca * cb;
-  const float cscale = pa.scale * p.w_scale;  // matrix.cc:404-405
+  i8_epilogue<TI, TJ, BM, 64 * NW>(p, acc, m0, wm * TI * 32, n0 + wn * TJ * 32, r, h, reinterpret_cast<uint32_t *>(smem));
+}
+
+
+// Register-staged form: the next K-tile is fetched with global_load_dwordx4
+// into VGPRs while the current one is multiplied, then written to the other
+// LDS buffer with ds_write_b128.  An LDS-DMA piece costs its wave ~60-180
+// issue cycles per KiB (MI355X_MICROARCH.md, per-instruction constants), and
+// an i8 MFMA consumes operands as fast as a bf16 one (1 KiB per 32 cycles),
+// so at 128 x 128 the DMA issue alone matched the MFMA time; a plain
+// 16-byte load + LDS write per KiB costs a few cycles.  One barrier per
+// K-tile: the buffer written at kt was last read at kt-1, before that
+// iteration's barrier.  BM x BN block tile, WGM x WGN waves, 128-byte
+// K-tiles, the same XOR chunk swizzle and fragment reads as above.
+template <int BM, int BN, int WGM, int WGN>
+__global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_i8_reg_kernel(I8Args p) {
+  constexpr int NT = 64 * WGM * WGN;
+  constexpr int BKB = 128;
+  constexpr int TI = BM / WGM / 32, TJ = BN / WGN / 32;
+  constexpr int LA = BM * 8 / NT, LB = BN * 8 / NT;  // 16-byte chunks per thread
+  constexpr int STAGE = (BM + BN) * BKB;
+  static_assert(LA * NT == BM * 8 && LB * NT == BN * 8 && TI >= 1 && TJ >= 1, "tile shape");
+  __shared__ __attribute__((aligned(16))) int8_t smem[2 * STAGE];
+  auto swz = [](int row) { return (row >> 1) & 7; };
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN, r = lane & 31, h = lane >> 5;
+  int tm, tn;
+  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // thread -> (row, chunk) of the tile: chunk = tid & 7 for every piece
+  const int chunk = tid & 7, row_base = tid >> 3;
+  constexpr int RSTEP = NT / 8;
+  uint32_t boff[LB], bdst[LB];
 #pragma unroll
-  for (int i = 0; i < TI; ++i) {
+  for (int j = 0; j < LB; ++j) {
+    const int row = row_base + j * RSTEP;
+    boff[j] = (uint32_t)(min(n0 + row, p.n - 1) * p.kpad + 16 * chunk);
+    bdst[j] = (uint32_t)(BM * BKB + row * BKB + 16 * (chunk ^ swz(row)));
+  }
+  uint32_t aoff[LA], adst[LA];
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int row = m0 + wm * TI * 32 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-      if (row >= p.m) continue;
-      uint32_t rs = 0;  // row sum of the spliced row
-      for (int sg = 0; sg < p.nseg; ++sg) {
-        int src = row + p.off[sg];
+  for (int i = 0; i < LA; ++i) {
+    const int row = row_base + i * RSTEP;
+    adst[i] = (uint32_t)(row * BKB + 16 * (chunk ^ swz(row)));
+  }
+  int cur_seg = -1;
+  i32x4 ra[LA], rb[LB];
+  auto fetch = [&](int kt) {
+    const int k0 = kt * BKB;
+    const int seg = k0 / p.din, col0 = k0 - seg * p.din;
+    if (seg != cur_seg) {
+      cur_seg = seg;
+      const int shift = p.off[seg < 8 ? seg : 7];
+#pragma unroll
+      for (int i = 0; i < LA; ++i) {
+        int src = m0 + row_base + i * RSTEP + shift;
         src = src < 0 ? 0 : (src > p.m - 1 ? p.m - 1 : src);
-        rs += (uint32_t)p.rowsum[src];
-      }
-#pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        const int col = n0 + wn * TJ * 32 + j * 32 + r;
-        if (col >= p.n) continue;
-        const uint32_t v = (uint32_t)acc[i][j][e] + cb * rs + ca * (uint32_t)p.colsum[col] + kterm;
-        float y = (float)(int32_t)v * cscale;
-        if (p.bias) y = y + p.bias[col];
-        for (int q = 0; q < p.npost; ++q) {
-          if (p.post[q] == kPostRelu) {
-            y = y < 0.0f ? 0.0f : y;
-          } else if (p.post[q] == kPostBatchNorm) {
-            y = y * p.bn_scale[col];
-            y = y + p.bn_offset[col];
-          }
-        }
-        p.y[(int64_t)row * p.ldy + col] = y;
+        aoff[i] = (uint32_t)(src * p.lda + 16 * chunk);
       }
     }
+    const int8_t *abase = p.a + col0;
+    const int8_t *bbase = p.w + k0;
+#pragma unroll
+    for (int i = 0; i < LA; ++i) ra[i] = *reinterpret_cast<const i32x4 *>(abase + aoff[i]);
+#pragma unroll
+    for (int j = 0; j < LB; ++j) rb[j] = *reinterpret_cast<const i32x4 *>(bbase + boff[j]);
+  };
+  auto stash = [&](int8_t *st) {
+#pragma unroll
+    for (int i = 0; i < LA; ++i) *reinterpret_cast<i32x4 *>(st + adst[i]) = ra[i];
+#pragma unroll
+    for (int j = 0; j < LB; ++j) *reinterpret_cast<i32x4 *>(st + bdst[j]) = rb[j];
+  };
+
+  i32x16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0;
+
+  const int xr = swz(r) ^ h;
+  const int a_row = (wm * TI * 32 + r) * BKB, b_row = BM * BKB + (wn * TJ * 32 + r) * BKB;
+  const int ktiles = p.kpad / BKB;
+  fetch(0);
+  stash(smem);
+  __syncthreads();
+  for (int kt = 0; kt < ktiles; ++kt) {
+    const bool more = kt + 1 < ktiles;
+    if (more) fetch(kt + 1);
+    const int8_t *st = smem + (kt & 1) * STAGE;
+#pragma unroll
+    for (int s = 0; s < BKB / 32; ++s) {
+      const int ch = ((2 * s) ^ xr) * 16;
+      i32x4 af[TI], bf[TJ];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) af[i] = *reinterpret_cast<const i32x4 *>(st + a_row + i * 32 * BKB + ch);
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) bf[j] = *reinterpret_cast<const i32x4 *>(st + b_row + j * 32 * BKB + ch);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) stash(smem + ((kt + 1) & 1) * STAGE);
+    __syncthreads();
   }
+  i8_epilogue<TI, TJ, BM, NT>(p, acc, m0, wm * TI * 32, n0 + wn * TJ * 32, r, h, reinterpret_cast<uint32_t *>(smem));
 }
 
 }  // namespace
@@ -502,11 +601,12 @@ int launch_i8_gemm(hipStream_t s, const I8Layer &L, const int8_t *a, int lda, in
   p.bn_offset = L.bn_offset;
   for (int i = 0; i < 4; ++i) p.post[i] = L.post[i];
   p.npost = L.npost;
+  p.post_mode = post_mode(L.post, L.npost);
   p.y = y;
   p.ldy = ldy;
   static const int use_glds = [] {
     const char *e = getenv("CATEARS_I8_GEMM");
-    return e ? atoi(e) : 9;  // measured best on TDNN-S, frame batch 8192 (scratch sweep)
+    return e ? atoi(e) : 15;  // measured best on TDNN-S, frame batch 8192 (tools/i8_sweep.sh)
   }();
   if (use_glds && p.kpad % 128 == 0 && p.din % 128 == 0 && lda % 16 == 0) {
     auto go = [&](auto kern, int bm, int bn, int threads = 256) {
@@ -527,6 +627,14 @@ int launch_i8_gemm(hipStream_t s, const I8Layer &L, const int8_t *a, int lda, in
       // DMA round trip per iteration, not by MFMA issue
       case 8: go(gemm_i8_glds_kernel<128, 256, 2, 2, 4>, 128, 256, 512); break;
       case 9: go(gemm_i8_glds_kernel<256, 256, 2, 4, 2>, 256, 256, 512); break;
+      case 10: go(gemm_i8_reg_kernel<128, 128, 2, 2>, 128, 128, 256); break;
+      case 11: go(gemm_i8_reg_kernel<256, 128, 4, 2>, 256, 128, 512); break;
+      // 15: 256 x 128, 3 stages (144 KiB), 8 waves of 64 x 64: one tile per
+      // CU on the 1024-wide layers and two K-tiles in flight.  The serial
+      // per-layer times of 1, 7, 10, 11 and 15 are within 5 % of each other
+      // (the loop waits on L2 / MALL fetches, 43 % of wave cycles parked, MFMA
+      // busy ~20 %); 9 (128 tiles) leaves half the CUs idle when alone.
+      case 15: go(gemm_i8_glds_kernel<256, 128, 3, 4, 2>, 256, 128, 512); break;
       default: go(gemm_i8_glds_kernel<128, 128, 2>, 128, 128); break;
     }
     CE_HIP(hipGetLastError());

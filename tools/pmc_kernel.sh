@@ -5,9 +5,10 @@ OUT=${OUT:-pmck}
 mkdir -p "$R/gpurun_out/$OUT"
 cd /tmp && export TMPDIR=/tmp
 i=0
-for grp in "SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU" \
-           "SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES" \
-           "SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY" ${EXTRA_GROUPS}; do
+# PGROUPS (';'-separated counter groups) replaces the default groups.
+DEFAULT_GROUPS="SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU;SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES;SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY"
+IFS=';' read -ra PG <<< "${PGROUPS:-$DEFAULT_GROUPS}"
+for grp in "${PG[@]}" ${EXTRA_GROUPS}; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "${KREGEX:-fbank}" --output-format csv \
       -d "$R/gpurun_out/$OUT/p$i" -o run -- \
