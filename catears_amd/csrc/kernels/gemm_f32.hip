@@ -44,12 +44,41 @@ struct KArgs {
   int din, nseg;
   uint64_t off_packed;  // splice offset of segment s in signed byte s
   int post[4];
-  int npost;
+  int npost, post_mode;
   int tiles_m, tiles_n;
   int group;  // column tiles per tile group (tile_of)
 };
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// Epilogue of one wave's (TI x 32) x (TJ x 32) tile at (row0, col0): + bias,
+// then the fused post-ops in model order with the reference's roundings
+// (add, then multiply and add separately -- built without FMA contraction).
+// An absent bias adds -0, an exact identity for every float (-0 included), so
+// the add is unconditional; the post chain is one uniform mode per launch.
+template <int TI, int TJ>
+__device__ __forceinline__ void f32_epilogue(const KArgs &p, const f32x16 (&acc)[TI][TJ], int row0, int col0, int r,
+                                             int h) {
+  with_post_mode(p.post_mode, [&](auto M) {
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int col = col0 + j * 32 + r;
+      if (col >= p.n) continue;
+      const float bias = p.bias ? p.bias[col] : -0.0f;
+      const float sc = p.bn_scale ? p.bn_scale[col] : 1.0f;
+      const float of = p.bn_offset ? p.bn_offset[col] : -0.0f;
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = row0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+          const float v = apply_post<decltype(M)::value>(acc[i][j][e] + bias, sc, of, p.post, p.npost);
+          if (row < p.m) p.y[(int64_t)row * p.ldy + col] = v;
+        }
+      }
+    }
+  });
+}
 
 // Tile configuration: BM x BN block tile, BK deep, WGM x WGN waves.
 template <int BM_, int BN_, int BK_, int WGM_, int WGN_>
@@ -242,36 +271,7 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_kernel(KArgs p) {
     __syncthreads();
   }
 
-  // Epilogue: + bias, then the fused post-ops in model order (reference
-  // roundings: add, then multiply and add separately -- built without FMA
-  // contraction).
-#pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    const int col = n0 + wn * TJ * 32 + j * 32 + r;
-    if (col >= p.n) continue;
-    const float bias = p.bias ? p.bias[col] : 0.0f;
-    const float sc = p.bn_scale ? p.bn_scale[col] : 1.0f;
-    const float of = p.bn_offset ? p.bn_offset[col] : 0.0f;
-#pragma unroll
-    for (int i = 0; i < TI; ++i) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int row = m0 + wm * TI * 32 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        if (row >= p.m) continue;
-        float v = acc[i][j][e];
-        if (p.bias) v = v + bias;
-        for (int q = 0; q < p.npost; ++q) {
-          if (p.post[q] == kPostRelu) {
-            v = v < 0.0f ? 0.0f : v;
-          } else if (p.post[q] == kPostBatchNorm) {
-            v = v * sc;
-            v = v + of;
-          }
-        }
-        p.y[(int64_t)row * p.ldy + col] = v;
-      }
-    }
-  }
+  f32_epilogue<TI, TJ>(p, acc, m0 + wm * TI * 32, n0 + wn * TJ * 32, r, h);
 }
 
 // Software-pipelined variant: fragments of k-group g+1 are read from LDS
@@ -357,33 +357,7 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_pipe_kernel(KArgs p) {
     // G is even, so the next tile's group 0 landed in fa0/fb0.
   }
 
-#pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    const int col = n0 + wn * TJ * 32 + j * 32 + r;
-    if (col >= p.n) continue;
-    const float bias = p.bias ? p.bias[col] : 0.0f;
-    const float sc = p.bn_scale ? p.bn_scale[col] : 1.0f;
-    const float of = p.bn_offset ? p.bn_offset[col] : 0.0f;
-#pragma unroll
-    for (int i = 0; i < TI; ++i) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int row = m0 + wm * TI * 32 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        if (row >= p.m) continue;
-        float v = acc[i][j][e];
-        if (p.bias) v = v + bias;
-        for (int q = 0; q < p.npost; ++q) {
-          if (p.post[q] == kPostRelu) {
-            v = v < 0.0f ? 0.0f : v;
-          } else if (p.post[q] == kPostBatchNorm) {
-            v = v * sc;
-            v = v + of;
-          }
-        }
-        p.y[(int64_t)row * p.ldy + col] = v;
-      }
-    }
-  }
+  f32_epilogue<TI, TJ>(p, acc, m0 + wm * TI * 32, n0 + wn * TJ * 32, r, h);
 }
 
 // Pipeline v2 (write-after-barrier, the register-staging schedule of the
@@ -469,33 +443,7 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_pipe2_kernel(KArgs p) {
     }
   }
 
-#pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    const int col = n0 + wn * TJ * 32 + j * 32 + r;
-    if (col >= p.n) continue;
-    const float bias = p.bias ? p.bias[col] : 0.0f;
-    const float sc = p.bn_scale ? p.bn_scale[col] : 1.0f;
-    const float of = p.bn_offset ? p.bn_offset[col] : 0.0f;
-#pragma unroll
-    for (int i = 0; i < TI; ++i) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int row = m0 + wm * TI * 32 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        if (row >= p.m) continue;
-        float v = acc[i][j][e];
-        if (p.bias) v = v + bias;
-        for (int q = 0; q < p.npost; ++q) {
-          if (p.post[q] == kPostRelu) {
-            v = v < 0.0f ? 0.0f : v;
-          } else if (p.post[q] == kPostBatchNorm) {
-            v = v * sc;
-            v = v + of;
-          }
-        }
-        p.y[(int64_t)row * p.ldy + col] = v;
-      }
-    }
-  }
+  f32_epilogue<TI, TJ>(p, acc, m0 + wm * TI * 32, n0 + wn * TJ * 32, r, h);
 }
 
 template <class C>
@@ -728,33 +676,7 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_f32_glds_kernel(KArgs p) {
     if (PRIO) __builtin_amdgcn_s_setprio(0);
   }
 
-#pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    const int col = n0 + wn * TJ * 32 + j * 32 + r;
-    if (col >= p.n) continue;
-    const float bias = p.bias ? p.bias[col] : 0.0f;
-    const float sc = p.bn_scale ? p.bn_scale[col] : 1.0f;
-    const float of = p.bn_offset ? p.bn_offset[col] : 0.0f;
-#pragma unroll
-    for (int i = 0; i < TI; ++i) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int row = m0 + wm * TI * 32 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        if (row >= p.m) continue;
-        float v = acc[i][j][e];
-        if (p.bias) v = v + bias;
-        for (int q = 0; q < p.npost; ++q) {
-          if (p.post[q] == kPostRelu) {
-            v = v < 0.0f ? 0.0f : v;
-          } else if (p.post[q] == kPostBatchNorm) {
-            v = v * sc;
-            v = v + of;
-          }
-        }
-        p.y[(int64_t)row * p.ldy + col] = v;
-      }
-    }
-  }
+  f32_epilogue<TI, TJ>(p, acc, m0 + wm * TI * 32, n0 + wn * TJ * 32, r, h);
 }
 
 // glds for the layers it fits, pipe2 for the rest (first layer's gather,
@@ -820,6 +742,7 @@ int launch_gemm_f32(hipStream_t s, const GemmArgs &a) {
   }
   for (int i = 0; i < 4; ++i) p.post[i] = a.post[i];
   p.npost = a.npost;
+  p.post_mode = post_mode(a.post, a.npost);
   static const int group_env = [] {
     const char *e = getenv("CATEARS_GEMM_GROUP");
     return e ? atoi(e) : 0;
