@@ -1201,6 +1201,25 @@ int ce_gpu_rowwise(ce_gpu_ctx *ctx, int op, int rows, int dim, float *d_x, int l
   return launch_rowop_raw(ctx->stream, op, dim, d_scale, d_offset, d_x, ld, rows);
 }
 
+int ce_gpu_loglik_gather(ce_gpu_ctx *ctx, const float *d_loglik, int rows, int ld, const int32_t *d_tid2pdf,
+                         int n_tid, const int32_t *d_row, const int32_t *d_trans, int n, float am_scale,
+                         float *d_out) {
+  if (!ctx || rows < 0 || ld < 0 || n_tid < 0 || n < 0) return fail(CE_GPU_EINVAL, "bad argument");
+  if (n == 0) return CE_GPU_OK;
+  if (!d_loglik || !d_tid2pdf || !d_row || !d_trans || !d_out) return fail(CE_GPU_EINVAL, "NULL argument");
+  CE_HIP(hipSetDevice(ctx->device));
+  return launch_loglik_gather(ctx->stream, d_loglik, rows, ld, d_tid2pdf, n_tid, d_row, d_trans, n, am_scale, d_out);
+}
+
+int ce_gpu_loglik_columns(ce_gpu_ctx *ctx, const float *d_loglik, int rows, int ld, int dim,
+                          const int32_t *d_cols, int n_cols, float *d_out) {
+  if (!ctx || rows < 0 || dim < 0 || ld < dim || n_cols < 0) return fail(CE_GPU_EINVAL, "bad argument");
+  if (rows == 0 || n_cols == 0) return CE_GPU_OK;
+  if (!d_loglik || !d_cols || !d_out) return fail(CE_GPU_EINVAL, "NULL argument");
+  CE_HIP(hipSetDevice(ctx->device));
+  return launch_loglik_columns(ctx->stream, d_loglik, rows, ld, dim, d_cols, n_cols, d_out);
+}
+
 int ce_gpu_model_quantize(ce_gpu_ctx *ctx, ce_gpu_model *m) {
   if (!ctx || !m) return fail(CE_GPU_EINVAL, "NULL argument");
   if (m->int8) return CE_GPU_OK;

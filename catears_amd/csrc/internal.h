@@ -303,6 +303,10 @@ int gemm_k_align();
 int launch_finalize(hipStream_t s, const float *x, int ldx, int rows, int dim, bool log_softmax,
                     const float *log_prior, const int *row_dst, float *out);
 int launch_rowop(hipStream_t s, const RowOp &op, float *x, int ldx, int rows);
+int launch_loglik_gather(hipStream_t s, const float *ll, int rows, int ld, const int32_t *tpm, int n_tid,
+                         const int32_t *row, const int32_t *trans, int n, float scale, float *out);
+int launch_loglik_columns(hipStream_t s, const float *ll, int rows, int ld, int dim, const int32_t *cols,
+                          int n_cols, float *out);
 int launch_rowop_raw(hipStream_t s, int kind, int dim, const float *scale, const float *offset, float *x,
                      int ldx, int rows);
 int launch_splice(hipStream_t s, int rows, int dim, const float *in, int ld_in, const int32_t *h_idx,

@@ -244,6 +244,57 @@ int launch_rowop_raw(hipStream_t s, int kind, int dim, const float *scale, const
   return CE_GPU_OK;
 }
 
+namespace {
+
+// One (frame, transition id) pair per thread: two dependent 4-byte reads
+// (the map, then the loglik element) -- latency, not bandwidth, so a wide
+// grid of small blocks.
+__global__ __launch_bounds__(256) void loglik_gather_kernel(const float *__restrict__ ll, int rows, int ld,
+                                                            const int32_t *__restrict__ tpm, int n_tid,
+                                                            const int32_t *__restrict__ row,
+                                                            const int32_t *__restrict__ trans, int n, float scale,
+                                                            float *__restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int r = row[i], t = trans[i];
+  float v = __builtin_nanf("");
+  if (r >= 0 && r < rows && t >= 0 && t < n_tid) v = scale * ll[(int64_t)r * ld + tpm[t]];
+  out[i] = v;
+}
+
+// out row r = the selected columns of ll row r; a block per row, the column
+// list read once per block into registers.
+__global__ __launch_bounds__(256) void loglik_columns_kernel(const float *__restrict__ ll, int ld, int dim,
+                                                             const int32_t *__restrict__ cols, int n_cols,
+                                                             float *__restrict__ out) {
+  const int r = blockIdx.x;
+  const float *src = ll + (int64_t)r * ld;
+  float *dst = out + (int64_t)r * n_cols;
+  for (int j = threadIdx.x; j < n_cols; j += 256) {
+    const int c = cols[j];
+    dst[j] = (c >= 0 && c < dim) ? src[c] : __builtin_nanf("");
+  }
+}
+
+}  // namespace
+
+int launch_loglik_gather(hipStream_t s, const float *ll, int rows, int ld, const int32_t *tpm, int n_tid,
+                         const int32_t *row, const int32_t *trans, int n, float scale, float *out) {
+  if (n > 0)
+    hipLaunchKernelGGL(loglik_gather_kernel, dim3((n + 255) / 256), dim3(256), 0, s, ll, rows, ld, tpm, n_tid, row,
+                       trans, n, scale, out);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
+int launch_loglik_columns(hipStream_t s, const float *ll, int rows, int ld, int dim, const int32_t *cols,
+                          int n_cols, float *out) {
+  if (rows > 0 && n_cols > 0)
+    hipLaunchKernelGGL(loglik_columns_kernel, dim3(rows), dim3(256), 0, s, ll, ld, dim, cols, n_cols, out);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
 int launch_rowop(hipStream_t s, const RowOp &op, float *x, int ldx, int rows) {
   return launch_rowop_raw(s, op.kind, op.dim, op.scale.as<float>(), op.offset.as<float>(), x, ldx, rows);
 }

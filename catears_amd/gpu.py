@@ -29,7 +29,7 @@ ABI = [
     "ce_gpu_gemm_u8u8f32", "ce_gpu_gemm_u8u8i32", "ce_gpu_model_load_mem",
     "ce_gpu_nnet_propagate", "ce_gpu_linear", "ce_gpu_splice", "ce_gpu_rowwise",
     "ce_gpu_profile_anchor", "ce_gpu_ctx_profile_intervals", "ce_gpu_model_quantize",
-    "ce_gpu_nnet_propagate_blocks",
+    "ce_gpu_nnet_propagate_blocks", "ce_gpu_loglik_gather", "ce_gpu_loglik_columns",
 ]
 
 _lib = None
@@ -88,6 +88,8 @@ def lib():
         "ce_gpu_linear": (ci, [vp, ci, ci, ci, vp, ci, vp, ci, vp, vp, ci]),
         "ce_gpu_splice": (ci, [vp, ci, ci, vp, ci, ctypes.POINTER(ctypes.c_int32), ci, vp]),
         "ce_gpu_rowwise": (ci, [vp, ci, ci, ci, vp, ci, vp, vp]),
+        "ce_gpu_loglik_gather": (ci, [vp, vp, ci, ci, vp, ci, vp, vp, ci, ctypes.c_float, vp]),
+        "ce_gpu_loglik_columns": (ci, [vp, vp, ci, ci, ci, vp, ci, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -325,6 +327,31 @@ def nnet_propagate_blocks(ctx, model, x, block_rows, subtract_prior=False, out=N
     check(lib().ce_gpu_nnet_propagate_blocks(ctx.h, model.h, _ptr(x), x.stride(0),
                                              rows.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), len(rows),
                                              int(subtract_prior), _ptr(out)))
+    return out
+
+
+def loglik_gather(ctx, loglik, tid2pdf, rows, trans, am_scale=1.0, out=None):
+    """ce_gpu_loglik_gather: am_scale * loglik[rows[i], tid2pdf[trans[i]]]
+    (Decoder::LogLikelihood for n pairs); int32 device tensors."""
+    import torch
+    n = int(rows.numel())
+    assert trans.numel() == n and rows.dtype == trans.dtype == tid2pdf.dtype == torch.int32
+    if out is None:
+        out = torch.empty((n,), dtype=torch.float32, device=loglik.device)
+    check(lib().ce_gpu_loglik_gather(ctx.h, _ptr(loglik), loglik.shape[0], loglik.stride(0), _ptr(tid2pdf),
+                                     int(tid2pdf.numel()), _ptr(rows), _ptr(trans), n, float(am_scale),
+                                     _ptr(out)))
+    return out
+
+
+def loglik_columns(ctx, loglik, cols, out=None):
+    """ce_gpu_loglik_columns: loglik[:, cols] compacted (int32 device cols)."""
+    import torch
+    assert cols.dtype == torch.int32
+    if out is None:
+        out = torch.empty((loglik.shape[0], int(cols.numel())), dtype=torch.float32, device=loglik.device)
+    check(lib().ce_gpu_loglik_columns(ctx.h, _ptr(loglik), loglik.shape[0], loglik.stride(0), loglik.shape[1],
+                                      _ptr(cols), int(cols.numel()), _ptr(out)))
     return out
 
 

@@ -270,6 +270,23 @@ int ce_gpu_splice(ce_gpu_ctx *ctx, int rows, int dim, const float *d_in, int ld_
 int ce_gpu_rowwise(ce_gpu_ctx *ctx, int op, int rows, int dim, float *d_x, int ld, const float *d_scale,
                    const float *d_offset);
 
+/* Decoder::LogLikelihood (src/decoder.cc:97-102) in bulk, on the device:
+ *   d_out[i] = am_scale * d_loglik[d_row[i] * ld + d_tid2pdf[d_trans[i]]]
+ * for n (frame, transition-id) pairs -- the acoustic costs of a frame's
+ * active arcs (ProcessEmitting, src/decoder.cc:327,350 negate them), so a
+ * decoder reads n floats instead of whole 3456-wide rows.  A pair whose frame
+ * is outside [0, rows) or whose transition id is outside [0, n_tid) yields
+ * NaN (the reference indexes out of bounds there). */
+int ce_gpu_loglik_gather(ce_gpu_ctx *ctx, const float *d_loglik, int rows, int ld, const int32_t *d_tid2pdf,
+                         int n_tid, const int32_t *d_row, const int32_t *d_trans, int n, float am_scale,
+                         float *d_out);
+
+/* Column subset of a log-likelihood block: d_out[r * n_cols + j] =
+ * d_loglik[r * ld + d_cols[j]] (NaN for a column outside [0, dim)) -- the
+ * pdfs a decoding graph can reach, compacted before the D2H copy. */
+int ce_gpu_loglik_columns(ce_gpu_ctx *ctx, const float *d_loglik, int rows, int ld, int dim,
+                          const int32_t *d_cols, int n_cols, float *d_out);
+
 #ifdef __cplusplus
 }  /* extern "C" */
 #endif

@@ -314,6 +314,16 @@ def gemm_u8u8f32(a, sa, zpa, b, sb, zpb):
     return c
 
 
+# --------------------------------------------------------------- decoder --
+
+def decoder_loglikelihood(frame_logp, tid2pdf, rows, trans, am_scale):
+    """Decoder::LogLikelihood (src/decoder.cc:97-102): am_scale * frame_logp[
+    tid2pdf[trans_id]], a float32 product, for each (frame row, transition
+    id) pair: frame_logp is (frames x pdfs), rows / trans index arrays."""
+    pdf = np.asarray(tid2pdf, np.int32)[np.asarray(trans)]
+    return (np.float32(am_scale) * np.asarray(frame_logp, np.float32)[np.asarray(rows), pdf]).astype(np.float32)
+
+
 # ------------------------------------------------------------------- wav --
 
 def read_wav(path):
