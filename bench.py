@@ -107,7 +107,8 @@ def cpu_baseline(conf, n_utts, seconds, threads, min_wall):
     return frames / dt, frames, dt, passes
 
 
-ROOFLINE_KERNEL = "gemm_f32_glds_kernel<catears::Cfg<128, 64, 32, 2, 2>, 2>"
+ROOFLINE_KERNEL = "gemm_f32_glds_kernel<catears::Cfg<128, 64, 32, 2, 2>, 2, false>"
+I8_ROOFLINE_KERNEL = "gemm_i8_glds_kernel<256, 128, 3, 4, 2>"  # CATEARS_I8_GEMM default (nnet_i8.hip)
 
 
 def gemm_algorithmic_bytes(rows, layers=((3072, 1024),) * 4 + ((1024, 1024), (1024, 3456))):
@@ -416,14 +417,14 @@ def main():
     if prof:
         ms, n, busy = prof["gemm"]
         if n and int8:
-            # every Linear layer is one gemm_i8_nnet launch (class GEMM)
+            # every Linear layer is one int8 GEMM launch (class GEMM)
             ops_per_launch = frames_per_step * FLOPS_PER_FRAME / (n / args.steps)
             achieved = ops_per_launch * n / (busy * 1e-3) / 1e12
-            traffic, src = pmc_traffic("gemm_i8_nnet_kernel", "c5")
+            traffic, src = pmc_traffic(I8_ROOFLINE_KERNEL, "c5")
             roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": MFMA_I8_PEAK_TOPS,
                         "unit": "TOP/s", "frac": round(achieved / MFMA_I8_PEAK_TOPS, 4),
                         "traffic": traffic, "traffic_source": src,
-                        "kernel": "gemm_i8_nnet_kernel (TDNN-S layers 1-7)",
+                        "kernel": I8_ROOFLINE_KERNEL + " (TDNN-S layers 1-7)",
                         "launches": n, "avg_launch_ms": round(ms / n, 4), "busy_ms": round(busy, 3),
                         "effective_ms_per_launch": round(busy / n, 4), "ops_per_launch": ops_per_launch}
         elif n:
