@@ -17,6 +17,7 @@ Prints ONE JSON line (rank 0).  See DESIGN.md "Measurement" for every field.
 """
 import argparse
 import json
+import re
 import os
 import sys
 import tempfile
@@ -123,7 +124,8 @@ def pmc_traffic(kernel, workload="c3"):
     of this same bench and workload); None if there is none."""
     import glob
     pattern = "r*_pmc_traffic.json" if workload == "c3" else f"r*_{workload}_pmc_traffic.json"
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", pattern))
+                   if workload != "c3" or not re.search(r"_c\d_pmc_traffic\.json$", f))
     if not files:
         return None, None
     data = json.load(open(files[-1]))
