@@ -21,9 +21,13 @@ KERNELS := $(wildcard $(SRC)/kernels/*.hip)
 HOSTSRC := $(SRC)/capi.cc $(SRC)/tables.cc
 OBJS := $(patsubst $(SRC)/kernels/%.hip,$(OBJ)/%.o,$(KERNELS)) \
         $(patsubst $(SRC)/%.cc,$(OBJ)/%.o,$(HOSTSRC))
-HDRS := include/catears_gpu.h $(SRC)/internal.h $(SRC)/fbank_ops.h $(SRC)/tile_order.h
+HDRS := include/catears_gpu.h $(SRC)/internal.h $(SRC)/fbank_ops.h $(SRC)/tile_order.h $(SRC)/lds_dma.h
 
 all: $(LIB) oracle
+
+# the bf16x6 GEMM's small per-lane arrays stay in registers (hipcc would
+# otherwise promote one into LDS at 1 block/CU: +36 KB of LDS traffic)
+$(OBJ)/gemm_bf16x6.o $(OBJ)/gemm_f16x3.o: HIPFLAGS += -mllvm -disable-promote-alloca-to-lds=1
 
 $(OBJ)/%.o: $(SRC)/kernels/%.hip $(HDRS)
 	@mkdir -p $(OBJ)

@@ -33,6 +33,11 @@ FLOPS_PER_FRAME = 2 * (200 * 1024 + 4 * 3072 * 1024 + 1024 * 1024 + 1024 * 3456)
 FLOPS_PER_FRAME_FAST = FLOPS_PER_FRAME - 2 * 200 * 1024
 MFMA_F32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: dense fp32 MFMA (= vector) peak
 MFMA_I8_PEAK_TOPS = 5000.0       # MI355X_MICROARCH.md: int8 MFMA = 2x the ~2.5 PF dense bf16 rate
+MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: ~2.5 PF dense bf16 / fp16 (no sparsity)
+# Split-plane GEMMs (ce_gpu_model_set_gemm): bf16x6 issues six bf16 MFMA
+# products per fp32 multiply-add, f16x3 three fp16 ones, so the kernel's
+# ceiling in fp32 (algorithmic) FLOP/s is the 16-bit dense peak / products.
+SPLIT_PRODUCTS = {"bf16x6": 6, "f16x3": 3}
 HBM_PEAK_GBS = 8000.0
 METRIC = "acoustic frames/sec (fbank->nnet posteriors), 16kHz, 1/2/4/8 GPU"
 
@@ -60,6 +65,9 @@ def parse():
                     help="c3: full pipeline fp32 (the headline metric); c2: batched fbank only, "
                          "1000 x 10 s utterances per step; c5: full pipeline with the int8 nnet path, "
                          "frame batch 8192")
+    ap.add_argument("--gemm", choices=["fp32", "bf16x6", "f16x3"], default=None,
+                    help="matrix-core form of the fp32 Linear layers (ce_gpu_model_set_gemm); default: "
+                         "the library's (f16x3: two scaled fp16 planes, three products, fp32-accurate)")
     ap.add_argument("--back-streams", type=int, default=3,
                     help="nnet streams; consecutive batches alternate between them so one batch's "
                          "wave-quantisation tail overlaps the next batch's layers")
@@ -109,6 +117,18 @@ def cpu_baseline(conf, n_utts, seconds, threads, min_wall):
 
 
 ROOFLINE_KERNEL = "gemm_f32_glds_kernel<catears::Cfg<128, 64, 32, 2, 2>, 2, false>"
+# split-plane hidden layers (split output), the default variants
+SPLIT_ROOFLINE_KERNEL = {
+    "bf16x6": "gemm_bf16x6_kernel<catears::X6Cfg<128, 128, 2, 4, 2>, true, 0>",
+    "f16x3": "gemm_f16x3_kernel<catears::X3Cfg<128, 128, 2, 4, 2, 64>, true>",
+}
+SPLIT_DTYPE = {
+    "bf16x6": "fp32 (bf16x6 GEMM: fp32 operands split exactly into 3 bf16 planes, 6 MFMA products, fp32 "
+              "accumulate; error vs oracle at the fp32-MFMA path's level, tests/test_gpu_parity.py)",
+    "f16x3": "fp32 (f16x3 GEMM: fp32 operands scaled by powers of two and split into 2 fp16 planes, 22-23 "
+             "significant bits, 3 MFMA products in 2 fp32 accumulators; error vs oracle at the fp32-MFMA "
+             "path's level, tests/test_gpu_parity.py)",
+}
 I8_ROOFLINE_KERNEL = "gemm_i8_glds_kernel<256, 128, 3, 4, 2>"  # CATEARS_I8_GEMM default (nnet_i8.hip)
 
 
@@ -116,6 +136,18 @@ def gemm_algorithmic_bytes(rows, layers=((3072, 1024),) * 4 + ((1024, 1024), (10
     """fp32 A (rows x K) + W (K x N) + C (rows x N) bytes of TDNN-S layers 2-7,
     per launch on average (one launch per layer)."""
     return sum(4 * (rows * k + k * n + rows * n) for k, n in layers) / len(layers)
+
+
+def split_algorithmic_bytes(rows, eb, layers=((256, 1024),) + ((3072, 1024),) * 4 + ((1024, 1024), (1024, 3456))):
+    """Split-plane GEMM operands per launch on average over TDNN-S layers
+    1-7: A and W at eb bytes per element (6: three bf16 planes, 4: two fp16
+    planes; A counted once per row and segment), hidden outputs written split,
+    the last as fp32."""
+    tot = 0
+    for i, (k, n) in enumerate(layers):
+        out = 4 if i == len(layers) - 1 else eb
+        tot += eb * rows * k + eb * k * n + out * rows * n
+    return tot / len(layers)
 
 
 def pmc_traffic(kernel, workload="c3"):
@@ -303,6 +335,9 @@ def main():
     ctx_f = gpu.Context(local, front) if not args.serial else ctx
     int8 = args.workload == "c5"
     model = gpu.Model(ctx, conf)
+    if args.gemm:
+        model.set_gemm(args.gemm)
+    split = None if int8 or model.gemm == "fp32" else model.gemm
     if int8:
         model.quantize(ctx)
     n_samp = int(16000 * args.seconds)
@@ -392,6 +427,8 @@ def main():
     if gat is not None:
         checksum += gat.checksum
     finite = bool(torch.isfinite(outs[0]).all().item())
+    # f16x3: no activation left the two-plane range in any batch
+    overflow = any(c.overflow() for c in set(ctxs + [ctx_f]))
 
     prof = {}
     if not args.no_profile:
@@ -429,6 +466,31 @@ def main():
                         "kernel": I8_ROOFLINE_KERNEL + " (TDNN-S layers 1-7)",
                         "launches": n, "avg_launch_ms": round(ms / n, 4), "busy_ms": round(busy, 3),
                         "effective_ms_per_launch": round(busy / n, 4), "ops_per_launch": ops_per_launch}
+        elif n and split:
+            # split-plane GEMM: every Linear (layer 1 included) is one launch
+            # of class GEMM.  `achieved` counts the algorithmic fp32 FLOPs
+            # (2 K N per frame); the kernel's ceiling is the 16-bit dense peak
+            # over the MFMA products each fp32 multiply-add costs; over the
+            # union of the launches' intervals as below.
+            prods = SPLIT_PRODUCTS[split]
+            peak = MFMA_BF16_PEAK_TFLOPS / prods
+            flops_per_launch = frames_per_step * FLOPS_PER_FRAME / (n / args.steps)
+            achieved = flops_per_launch * n / (busy * 1e-3) / 1e12
+            traffic, src = pmc_traffic(SPLIT_ROOFLINE_KERNEL[split])
+            roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1),
+                        "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                        "peak_basis": f"{'bf16' if split == 'bf16x6' else 'fp16'} dense MFMA "
+                                      f"{MFMA_BF16_PEAK_TFLOPS:g} TFLOP/s / {prods} MFMA products per fp32 "
+                                      "multiply-add (achieved = fp32 algorithmic FLOPs)",
+                        "mfma_16bit_tflops": round(achieved * prods, 1),
+                        "vs_fp32_mfma_peak": round(achieved / MFMA_F32_PEAK_TFLOPS, 4),
+                        "traffic": traffic, "traffic_source": src,
+                        "kernel": SPLIT_ROOFLINE_KERNEL[split] + " (TDNN-S layers 1-7)",
+                        "launches": n, "avg_launch_ms": round(ms / n, 4), "busy_ms": round(busy, 3),
+                        "effective_ms_per_launch": round(busy / n, 4),
+                        "flops_per_launch": flops_per_launch,
+                        "algorithmic_bytes_per_launch": split_algorithmic_bytes(
+                            plan.max_chunk_rows, {"bf16x6": 6, "f16x3": 4}[split])}
         elif n:
             # With several nnet streams, launches of this kernel overlap each
             # other; a launch's own duration then includes time shared with
@@ -482,7 +544,8 @@ def main():
         "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "u8 x u8 -> int32 (fp32 features, epilogues, log-softmax)" if int8 else "fp32",
+        "dtype": ("u8 x u8 -> int32 (fp32 features, epilogues, log-softmax)" if int8 else
+                  SPLIT_DTYPE[split] if split else "fp32"),
         "data": "synthetic (seeded 16 kHz PCM, random-init TDNN-S in NN02 format)",
         "config": {"workload": ("C5 full pipeline with the int8 nnet path (Quantize + MatMat_U8U8F32 per "
                                 f"Linear), frame batch <= {max_rows} rows " if int8 else
@@ -495,9 +558,12 @@ def main():
                    "gather": gather},
         "roofline": roofline, "cpu_baseline": cpu, "stages": stages,
         "end_to_end_mfma_frac": round(value / world * FLOPS_PER_FRAME / 1e12 /
-                                      (MFMA_I8_PEAK_TOPS if int8 else MFMA_F32_PEAK_TFLOPS), 4),
+                                      (MFMA_I8_PEAK_TOPS if int8 else
+                                       MFMA_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS[split] if split else
+                                       MFMA_F32_PEAK_TFLOPS), 4),
+        "gemm_mode": "int8" if int8 else model.gemm,
         "int8_vs_fp32": accuracy,
-        "checksum": float(checksum.item()), "finite": finite,
+        "checksum": float(checksum.item()), "finite": finite, "split_overflow": overflow,
     }
     print(json.dumps(line), flush=True)
     if world > 1:

@@ -8,6 +8,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cctype>
 #include <fstream>
 #include <map>
@@ -269,7 +270,116 @@ static int read_nnet(Reader &rd, std::vector<RawLayer> *layers, int *hl, int *hr
 // (tool/convert_am.py:272-285); under that shape the output of a chunk does
 // not depend on where the chunk boundaries are, which is what lets the GPU run
 // whole utterances.  Other shapes are rejected with CE_GPU_ENOTSUP.
+// fp32 -> bf16, round to nearest even (v_cvt_pk_bf16_f32; NaN stays NaN).
+static uint16_t bf16_rne(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+static float bf16_float(uint16_t h) {
+  const uint32_t u = (uint32_t)h << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+// The bf16x6 GEMM's weight image: row j of the n x kpad matrix as three bf16
+// planes [w0 | w1 | w2], w = w0 + w1 + w2 (kernels/gemm_bf16x6.hip).
+static int upload_split(const std::vector<float> &wt, int n, int kpad, DevBuf *out) {
+  std::vector<uint16_t> sp((size_t)n * 3 * kpad);
+  for (int j = 0; j < n; ++j)
+    for (int k = 0; k < kpad; ++k) {
+      const float v = wt[(size_t)j * kpad + k];
+      const uint16_t h = bf16_rne(v);
+      const float r1 = v - bf16_float(h);
+      const uint16_t m = bf16_rne(r1);
+      const float r2 = r1 - bf16_float(m);
+      uint16_t *row = sp.data() + (size_t)j * 3 * kpad;
+      row[k] = h;
+      row[kpad + k] = m;
+      row[2 * kpad + k] = bf16_rne(r2);
+    }
+  return out->upload(sp.data(), sp.size() * 2);
+}
+
+// fp32 -> fp16 bits, round to nearest even (v_cvt_f16_f32), inf beyond 65504.
+static uint16_t f16_rne(float f) {
+  uint32_t x;
+  memcpy(&x, &f, 4);
+  const uint16_t sign = (uint16_t)((x >> 16) & 0x8000u);
+  const uint32_t a = x & 0x7fffffffu;
+  if (a >= 0x7f800000u) return sign | 0x7c00u | (a > 0x7f800000u ? 0x200u : 0u);
+  if (a >= 0x477ff000u) return sign | 0x7c00u;  // >= 65520 rounds to infinity
+  if (a < 0x38800000u) {                          // below 2^-14: subnormal
+    float v;
+    memcpy(&v, &a, 4);
+    return sign | (uint16_t)nearbyintf(v * 16777216.0f);  // units of 2^-24
+  }
+  const uint32_t r = a - 0x38000000u;  // rebias 127 -> 15
+  return sign | (uint16_t)((r + 0xfffu + ((r >> 13) & 1u)) >> 13);
+}
+static float f16_float(uint16_t h) {
+  const uint32_t sign = (uint32_t)(h & 0x8000u) << 16, e = (h >> 10) & 31u, m = h & 0x3ffu;
+  float v;
+  if (e == 0) {
+    v = ldexpf((float)m, -24);
+  } else if (e == 31) {
+    const uint32_t u = 0x7f800000u | (m << 13);
+    memcpy(&v, &u, 4);
+  } else {
+    const uint32_t u = ((e + 112u) << 23) | (m << 13);
+    memcpy(&v, &u, 4);
+  }
+  uint32_t u;
+  memcpy(&u, &v, 4);
+  u |= sign;
+  memcpy(&v, &u, 4);
+  return v;
+}
+
+// The f16x3 GEMM's weight image (kernels/gemm_f16x3.hip): u = w * 2^shift
+// with max |u| in [2^14, 2^15), row j = [f16(u) | f16((u - f16(u)) * 2^11)].
+// Returns false (image not built) when the weights are not all finite.
+static int upload_f16(const std::vector<float> &wt, int n, int kpad, DevBuf *out, int *shift, bool *ok) {
+  float mx = 0.0f;
+  for (float v : wt) {
+    if (!std::isfinite(v)) {
+      *ok = false;
+      return CE_GPU_OK;
+    }
+    mx = std::max(mx, std::fabs(v));
+  }
+  int e = 0;
+  if (mx > 0.0f) frexpf(mx, &e);  // mx in [2^(e-1), 2^e)
+  *shift = std::max(-100, std::min(100, 15 - e));
+  std::vector<uint16_t> sp((size_t)n * 2 * kpad);
+  for (int j = 0; j < n; ++j)
+    for (int k = 0; k < kpad; ++k) {
+      const float u = ldexpf(wt[(size_t)j * kpad + k], *shift);
+      const uint16_t h = f16_rne(u);
+      uint16_t *row = sp.data() + (size_t)j * 2 * kpad;
+      row[k] = h;
+      row[kpad + k] = f16_rne((u - f16_float(h)) * 2048.0f);
+    }
+  *ok = true;
+  return out->upload(sp.data(), sp.size() * 2);
+}
+
+// Default matrix-core form of the fp32 program (CATEARS_NNET_GEMM overrides).
+static int default_gemm() {
+  static const int g = [] {
+    const char *e = getenv("CATEARS_NNET_GEMM");
+    if (e && !strcmp(e, "fp32")) return (int)CE_GPU_GEMM_FP32;
+    if (e && !strcmp(e, "bf16x6")) return (int)CE_GPU_GEMM_BF16X6;
+    if (e && !strcmp(e, "f16x3")) return (int)CE_GPU_GEMM_F16X3;
+    return (int)CE_GPU_GEMM_F16X3;
+  }();
+  return g;
+}
+
 static int build_program(const std::vector<RawLayer> &layers, int left, int right, ce_gpu_model *m) {
+  m->x3_ok = true;           // cleared by a weight matrix the f16 planes cannot hold
   std::vector<int> pending;  // splice offsets waiting for their Linear
   bool have_pending = false, gemm_open = false;
   int width = -1, sum_l = 0, sum_r = 0, pend_l = 0, pend_r = 0;
@@ -321,6 +431,10 @@ static int build_program(const std::vector<RawLayer> &layers, int left, int righ
         for (int k = 0; k < in; ++k)
           for (int j = 0; j < out; ++j) wt[(size_t)j * g.kpad + k] = L.w[(size_t)k * out + j];
         CE_TRY(g.wt.upload(wt.data(), wt.size() * 4));
+        CE_TRY(upload_split(wt, out, g.kpad, &g.wsplit));
+        bool f16_ok = false;
+        CE_TRY(upload_f16(wt, out, g.kpad, &g.wf16, &g.w_shift, &f16_ok));
+        if (!f16_ok) m->x3_ok = false;
         CE_TRY(g.bias.upload(L.b.data(), L.b.size() * 4));
         m->num_params += (int64_t)in * out + out;
         m->max_width = std::max(m->max_width, out);
@@ -390,6 +504,20 @@ static int build_program(const std::vector<RawLayer> &layers, int left, int righ
     return fail(CE_GPU_ECORRUPT, fmt("Corruption: config context (%d, %d) differs from the nnet's (%d, %d)",
                                      left, right, sum_l, sum_r));
   m->num_pdfs = width;
+  // bf16x6 program: every step a Linear with its ReLU / BatchNorm fused, a
+  // K-tile of 32 inside one splice segment after the first layer (whose
+  // spliced block is written padded), output widths multiples of 4
+  m->x6_ok = true;
+  for (size_t i = 0; i < m->steps.size(); ++i) {
+    const Step &st = m->steps[i];
+    if (!st.is_gemm || st.gemm.n % 4 != 0 || (i > 0 && st.gemm.din % 32 != 0) || st.gemm.kpad % 32 != 0)
+      m->x6_ok = false;
+  }
+  m->x3_ok = m->x3_ok && m->x6_ok;
+  const int want = default_gemm();
+  m->gemm = want == CE_GPU_GEMM_F16X3 && m->x3_ok   ? CE_GPU_GEMM_F16X3
+            : want != CE_GPU_GEMM_FP32 && m->x6_ok ? CE_GPU_GEMM_BF16X6
+                                                    : CE_GPU_GEMM_FP32;
   return CE_GPU_OK;
 }
 
@@ -529,6 +657,17 @@ int ce_gpu_ctx_set_stream(ce_gpu_ctx *ctx, void *stream) {
   return CE_GPU_OK;
 }
 
+int ce_gpu_ctx_overflow(ce_gpu_ctx *ctx, int *overflow) {
+  if (!ctx || !overflow) return fail(CE_GPU_EINVAL, "NULL argument");
+  *overflow = 0;
+  if (!ctx->overflow.ptr) return CE_GPU_OK;
+  CE_HIP(hipSetDevice(ctx->device));
+  CE_HIP(hipStreamSynchronize(ctx->stream));
+  CE_HIP(hipMemcpy(overflow, ctx->overflow.ptr, sizeof(int), hipMemcpyDeviceToHost));
+  CE_HIP(hipMemset(ctx->overflow.ptr, 0, sizeof(int)));
+  return CE_GPU_OK;
+}
+
 int ce_gpu_ctx_synchronize(ce_gpu_ctx *ctx) {
   if (!ctx) return fail(CE_GPU_EINVAL, "ctx is NULL");
   CE_HIP(hipStreamSynchronize(ctx->stream));
@@ -645,6 +784,24 @@ int ce_gpu_model_info(const ce_gpu_model *m, int *left_context, int *right_conte
   if (num_pdfs) *num_pdfs = m->num_pdfs;
   if (num_linear) *num_linear = m->num_linear;
   if (num_params) *num_params = m->num_params;
+  return CE_GPU_OK;
+}
+
+int ce_gpu_model_set_gemm(ce_gpu_model *m, int mode) {
+  if (!m) return fail(CE_GPU_EINVAL, "NULL model");
+  if (mode != CE_GPU_GEMM_FP32 && mode != CE_GPU_GEMM_BF16X6 && mode != CE_GPU_GEMM_F16X3)
+    return fail(CE_GPU_EINVAL, "unknown GEMM mode");
+  if (mode != CE_GPU_GEMM_FP32 && !m->x6_ok)
+    return fail(CE_GPU_ENOTSUP, "this nnet program cannot run on split planes (unfused row op or widths)");
+  if (mode == CE_GPU_GEMM_F16X3 && !m->x3_ok)
+    return fail(CE_GPU_ENOTSUP, "a weight matrix is not finite: no f16x3 image");
+  m->gemm = mode;
+  return CE_GPU_OK;
+}
+
+int ce_gpu_model_get_gemm(const ce_gpu_model *m, int *mode) {
+  if (!m || !mode) return fail(CE_GPU_EINVAL, "NULL argument");
+  *mode = m->gemm;
   return CE_GPU_OK;
 }
 
@@ -867,6 +1024,158 @@ static int run_steps_f32(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
   *ldy = ldx;
   return CE_GPU_OK;
 }
+// The bf16x6 program (kernels/gemm_bf16x6.hip): the first layer's spliced
+// block is written as three bf16 planes, every hidden layer's epilogue
+// writes its output split for the next, the last layer writes fp32.
+static int run_steps_x6(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, int ldx, int rows,
+                        const int *row_map, const float **y, int *ldy) {
+  int max_in = 0;
+  for (const Step &st : m->steps) max_in = std::max(max_in, st.gemm.kpad);
+  for (const Step &st : m->steps) max_in = std::max(max_in, (st.gemm.n + 31) / 32 * 32);
+  // two split ping-pong blocks (rows x 3 x max_in bf16) + the fp32 output
+  const size_t split_floats = ((size_t)rows * 3 * max_in + 1) / 2;
+  const size_t split_stride = (split_floats + 63) / 64 * 64;
+  CE_TRY(ensure_workspace(ctx, 2 * split_stride + (size_t)rows * m->num_pdfs));
+  uint16_t *sbuf[2] = {reinterpret_cast<uint16_t *>(ctx->workspace.as<float>()),
+                       reinterpret_cast<uint16_t *>(ctx->workspace.as<float>() + split_stride)};
+  float *out = ctx->workspace.as<float>() + 2 * split_stride;
+  const uint16_t *xs = nullptr;
+  int px = 0;
+  int cur = 0;
+  for (size_t i = 0; i < m->steps.size(); ++i) {
+    const GemmLayer &g = m->steps[i].gemm;
+    const bool last = i + 1 == m->steps.size();
+    X6Gemm a;
+    if (i == 0) {
+      ProfScope prof(ctx, CE_GPU_PROF_GEMM_GATHER);
+      CE_TRY(launch_splice_pad_split(ctx->stream, x, ldx, rows, g.din, g.nseg, g.off, row_map, sbuf[cur], g.kpad));
+      xs = sbuf[cur];
+      px = g.kpad;
+      cur ^= 1;
+      a.din = g.kpad;
+      a.nseg = 1;
+    } else {
+      a.din = g.din;
+      a.nseg = g.nseg;
+      for (int s = 0; s < 8; ++s) a.off[s] = g.off[s];
+    }
+    a.x = xs;
+    a.ldx = 3 * px;
+    a.px = px;
+    a.w = g.wsplit.as<uint16_t>();
+    a.ldw = 3 * g.kpad;
+    a.pw = g.kpad;
+    a.m = rows;
+    a.n = g.n;
+    a.kpad = i == 0 ? g.kpad : g.nseg * g.din;
+    a.bias = g.bias.as<float>();
+    a.bn_scale = g.bn_scale.as<float>();
+    a.bn_offset = g.bn_offset.as<float>();
+    for (int q = 0; q < 4; ++q) a.post[q] = g.post[q];
+    a.npost = g.npost;
+    const int pn = (g.n + 31) / 32 * 32;
+    if (last) {
+      a.y32 = out;
+      a.ldy = g.n;
+    } else {
+      a.y16 = sbuf[cur];
+      a.ldy = 3 * pn;
+      a.py = pn;
+    }
+    {
+      ProfScope prof(ctx, CE_GPU_PROF_GEMM);
+      CE_TRY(launch_gemm_bf16x6(ctx->stream, a));
+    }
+    xs = sbuf[cur];
+    px = pn;
+    cur ^= 1;
+  }
+  *y = out;
+  *ldy = m->steps.back().gemm.n;
+  return CE_GPU_OK;
+}
+
+static int ensure_overflow_word(ce_gpu_ctx *ctx) {
+  if (ctx->overflow.ptr) return CE_GPU_OK;
+  CE_TRY(ctx->overflow.alloc(256));
+  CE_HIP(hipMemsetAsync(ctx->overflow.ptr, 0, 256, ctx->stream));
+  return CE_GPU_OK;
+}
+
+// The f16x3 program (kernels/gemm_f16x3.hip): as run_steps_x6 with two fp16
+// planes per operand; splits beyond the fp16 range set ctx->overflow.
+static int run_steps_x3(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, int ldx, int rows,
+                        const int *row_map, const float **y, int *ldy) {
+  CE_TRY(ensure_overflow_word(ctx));
+  int *overflow = ctx->overflow.as<int>();
+  int max_in = 0;
+  for (const Step &st : m->steps) max_in = std::max(max_in, st.gemm.kpad);
+  for (const Step &st : m->steps) max_in = std::max(max_in, (st.gemm.n + 63) / 64 * 64);
+  // two split ping-pong blocks (rows x 2 x max_in fp16) + the fp32 output
+  const size_t split_floats = (size_t)rows * max_in;
+  const size_t split_stride = (split_floats + 63) / 64 * 64;
+  CE_TRY(ensure_workspace(ctx, 2 * split_stride + (size_t)rows * m->num_pdfs));
+  uint16_t *sbuf[2] = {reinterpret_cast<uint16_t *>(ctx->workspace.as<float>()),
+                       reinterpret_cast<uint16_t *>(ctx->workspace.as<float>() + split_stride)};
+  float *out = ctx->workspace.as<float>() + 2 * split_stride;
+  const uint16_t *xs = nullptr;
+  int px = 0, cur = 0;
+  for (size_t i = 0; i < m->steps.size(); ++i) {
+    const GemmLayer &g = m->steps[i].gemm;
+    const bool last = i + 1 == m->steps.size();
+    X3Gemm a;
+    if (i == 0) {
+      ProfScope prof(ctx, CE_GPU_PROF_GEMM_GATHER);
+      CE_TRY(launch_splice_pad_f16(ctx->stream, x, ldx, rows, g.din, g.nseg, g.off, row_map, sbuf[cur], g.kpad,
+                                   overflow));
+      xs = sbuf[cur];
+      px = g.kpad;
+      cur ^= 1;
+      a.din = g.kpad;
+      a.nseg = 1;
+    } else {
+      a.din = g.din;
+      a.nseg = g.nseg;
+      for (int s = 0; s < 8; ++s) a.off[s] = g.off[s];
+    }
+    a.x = xs;
+    a.ldx = 2 * px;
+    a.px = px;
+    a.w = g.wf16.as<uint16_t>();
+    a.ldw = 2 * g.kpad;
+    a.pw = g.kpad;
+    a.m = rows;
+    a.n = g.n;
+    a.kpad = i == 0 ? g.kpad : g.nseg * g.din;
+    a.unscale = ldexpf(1.0f, -(g.w_shift + kF16ActShift));
+    a.bias = g.bias.as<float>();
+    a.bn_scale = g.bn_scale.as<float>();
+    a.bn_offset = g.bn_offset.as<float>();
+    for (int q = 0; q < 4; ++q) a.post[q] = g.post[q];
+    a.npost = g.npost;
+    a.overflow = overflow;
+    const int pn = (g.n + 63) / 64 * 64;
+    if (last) {
+      a.y32 = out;
+      a.ldy = g.n;
+    } else {
+      a.y16 = sbuf[cur];
+      a.ldy = 2 * pn;
+      a.py = pn;
+    }
+    {
+      ProfScope prof(ctx, CE_GPU_PROF_GEMM);
+      CE_TRY(launch_gemm_f16x3(ctx->stream, a));
+    }
+    xs = sbuf[cur];
+    px = pn;
+    cur ^= 1;
+  }
+  *y = out;
+  *ldy = m->steps.back().gemm.n;
+  return CE_GPU_OK;
+}
+
 // The int8 program (kernels/nnet_i8.hip): per Linear layer min/max ->
 // quantize (+ row sums) -> u8 GEMM with float epilogue.
 static int run_steps_i8(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, int ldx, int rows,
@@ -921,8 +1230,10 @@ static int run_steps_i8(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, 
 
 static int run_steps(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, int ldx, int rows,
                      const int *row_map, const uint32_t *row_edge, const float **y, int *ldy) {
-  return m->int8 ? run_steps_i8(ctx, m, x, ldx, rows, row_map, row_edge, y, ldy)
-                 : run_steps_f32(ctx, m, x, ldx, rows, row_map, y, ldy);
+  if (m->int8) return run_steps_i8(ctx, m, x, ldx, rows, row_map, row_edge, y, ldy);
+  if (m->gemm == CE_GPU_GEMM_F16X3) return run_steps_x3(ctx, m, x, ldx, rows, row_map, y, ldy);
+  if (m->gemm == CE_GPU_GEMM_BF16X6) return run_steps_x6(ctx, m, x, ldx, rows, row_map, y, ldy);
+  return run_steps_f32(ctx, m, x, ldx, rows, row_map, y, ldy);
 }
 
 // Quantize (src/matrix.cc:329-387) of one weight matrix on the host at load

@@ -155,6 +155,9 @@ struct GemmLayer {
   int off[8] = {0};       // row offset of each segment
   int k = 0, kpad = 0, n = 0;
   DevBuf wt;              // n x kpad, K-contiguous (transposed MAT0)
+  DevBuf wsplit;          // n x 3*kpad bf16: wt as three planes (bf16x6 GEMM)
+  DevBuf wf16;            // n x 2*kpad fp16: wt * 2^w_shift as two planes (f16x3 GEMM)
+  int w_shift = 0;
   DevBuf bias;            // n
   DevBuf bn_scale, bn_offset;  // n, when a BatchNorm is fused
   int post[4] = {0, 0, 0, 0};
@@ -215,6 +218,7 @@ struct ce_gpu_ctx {
   size_t workspace_floats = 0;
   catears::DevBuf scratch;     // reductions / int8 operand staging (grown on demand)
   catears::DevBuf blk_maps;    // ce_gpu_nnet_propagate_blocks: row_dst + row_edge
+  catears::DevBuf overflow;    // int: an f16x3 split left the fp16 range (ce_gpu_ctx_overflow)
   std::vector<int32_t> h_blk_maps;
   // optional per-class launch timing (ce_gpu_ctx_profile)
   bool profiling = false;
@@ -244,6 +248,9 @@ struct ce_gpu_model {
   int64_t num_params = 0;
   bool final_log_softmax = false;
   bool int8 = false;                 // Linear layers run as Quantize + u8 GEMM
+  int gemm = 0;                      // CE_GPU_GEMM_* for the fp32 program
+  bool x6_ok = false;                // program shape the bf16x6 / f16x3 paths take
+  bool x3_ok = false;                // ... and every weight fits the f16x3 planes
   std::vector<catears::Step> steps;  // all but the final log-softmax
   catears::DevBuf log_prior;         // num_pdfs
   std::vector<int32_t> tid2pdf;
@@ -297,6 +304,57 @@ struct GemmArgs {
 int launch_gemm_f32(hipStream_t s, const GemmArgs &a);
 // Weights' K dimension is zero-padded to a multiple of this (every tile variant's BK).
 int gemm_k_align();
+
+// fp32-accurate GEMM on the bf16 matrix cores (kernels/gemm_bf16x6.hip):
+// operands as three bf16 planes, six MFMA products.  x: rows x ldx, plane
+// stride px, read through the splice offsets (K-tile of 32 inside one
+// segment); w: n x ldw, plane stride pw (zero padded to kpad); output split
+// (y16, plane stride py) or fp32 (y32).
+struct X6Gemm {
+  const uint16_t *x = nullptr;
+  int ldx = 0, px = 0;
+  const uint16_t *w = nullptr;
+  int ldw = 0, pw = 0;
+  int m = 0, n = 0, kpad = 0, din = 0, nseg = 1;
+  int off[8] = {0};
+  const float *bias = nullptr, *bn_scale = nullptr, *bn_offset = nullptr;
+  int post[4] = {0, 0, 0, 0};
+  int npost = 0;
+  float *y32 = nullptr;
+  uint16_t *y16 = nullptr;
+  int ldy = 0, py = 0;
+};
+int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a);
+// splice_pad (below) written as three bf16 planes of width po: out row r at
+// out + r * 3 * po.
+int launch_splice_pad_split(hipStream_t s, const float *in, int ld_in, int rows, int din, int nseg, const int *off,
+                            const int *row_map, uint16_t *out, int po);
+
+// fp32-accurate GEMM on the fp16 matrix cores (kernels/gemm_f16x3.hip):
+// operands as two scaled fp16 planes, three MFMA products; same geometry as
+// X6Gemm with two planes.  unscale = 2^-(weight shift + activation shift);
+// overflow: device word set when a split output leaves the fp16 range.
+struct X3Gemm {
+  const uint16_t *x = nullptr;
+  int ldx = 0, px = 0;
+  const uint16_t *w = nullptr;
+  int ldw = 0, pw = 0;
+  int m = 0, n = 0, kpad = 0, din = 0, nseg = 1;
+  int off[8] = {0};
+  float unscale = 1.0f;
+  const float *bias = nullptr, *bn_scale = nullptr, *bn_offset = nullptr;
+  int post[4] = {0, 0, 0, 0};
+  int npost = 0;
+  float *y32 = nullptr;
+  uint16_t *y16 = nullptr;
+  int ldy = 0, py = 0;
+  int *overflow = nullptr;
+};
+int launch_gemm_f16x3(hipStream_t s, const X3Gemm &a);
+int launch_splice_pad_f16(hipStream_t s, const float *in, int ld_in, int rows, int din, int nseg, const int *off,
+                          const int *row_map, uint16_t *out, int po, int *overflow);
+// activations enter the f16x3 GEMM as x * 2^kF16ActShift
+constexpr int kF16ActShift = -8;
 
 // Final step: optional log-softmax per row, minus log prior, scatter to the
 // output rows named by row_dst (-1 = drop).

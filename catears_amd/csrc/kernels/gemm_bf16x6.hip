@@ -1,0 +1,555 @@
+// gemm_bf16x6.hip -- the TDNN layers' fp32 GEMM on the bf16 matrix cores.
+//
+// Same contraction as gemm_f32.hip (Splice + Narrow + LinearLayer + bias /
+// ReLU / BatchNorm, src/nnet.cc:22-43,50-75,106-117,149-160,182-202;
+// MatMat -> cblas_sgemm, src/matrix.cc:300-323), computed to fp32 accuracy
+// with v_mfma_f32_16x16x32_bf16:
+//
+//   every fp32 operand x is stored as three bf16 planes x = x0 + x1 + x2
+//   (x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1); each
+//   subtraction is exact, and 3 x 8 significand bits plus the signs cover
+//   fp32's 24, so the split is exact for every normal fp32 value), and
+//
+//   w . x = w0x0 + w0x1 + w1x0 + w1x1 + w0x2 + w2x0  (+ w1x2 + w2x1 + w2x2)
+//
+// The six kept products are exact in the MFMA (8 x 8 significand bits) and
+// accumulate in fp32; the three dropped ones are below 2^-25 |w x| each,
+// under the 2^-24 rounding of a single fp32 multiply.  So the result is an
+// fp32 GEMM with a different (blocked) summation order -- the same status as
+// the fp32-MFMA kernel -- at 6 bf16 MFMAs per fp32 MAC block: the bf16 rate
+// is 16x the fp32 MFMA rate on gfx950, i.e. 2.7x the fp32 ceiling.
+//
+// Layout (HBM):
+//   weights  n x ldw bf16, row j = [plane0 | plane1 | plane2], plane stride pw
+//            (= kpad, zero padded), uploaded once (capi.cc split_weights)
+//   acts     rows x ldx bf16, row r = [plane0 | plane1 | plane2], stride px;
+//            written split by the previous layer's epilogue (or by
+//            splice_pad_split for the first layer)
+//   output   split bf16 (a hidden layer) or fp32 (the last layer, which
+//            finalize reads)
+//
+// The MFMA's A operand is the weights (M = output units), B the activations
+// (N = frames): the accumulator then holds four consecutive units of one
+// frame per lane, so the epilogue reads bias/BN as float4 and stores 8 bytes
+// per plane (16 for fp32) per lane.
+//
+// Tiling: BW units x BF frames per block, K-tile 32 (one MFMA k-step, 64 B
+// per row per plane), 4 waves of (BW/2) x (BF/2).  Operands travel global ->
+// LDS by LDS-DMA (global_load_lds_dwordx4: one wave instruction = 16 rows x
+// 64 B of one plane), STAGES-deep ring, one barrier per K-tile, counted
+// vmcnt (same protocol as gemm_f32_glds_kernel).  Bank spread: 16-B chunk c
+// of tile row r is stored at chunk c ^ (2 * ((r >> 3) & 1)), applied on the
+// source address; each of ds_read_b128's four 16-lane groups ({0-3,12-15,
+// 20-27}, {4-11,16-19,28-31}, +32) then hits 16 distinct bank slots
+// (MI355X_MICROARCH.md, LDS; the plain (r >> 2) & 3 swizzle is 2-way there).
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+
+#include "../internal.h"
+#include "../tile_order.h"
+
+namespace catears {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct X6Args {
+  const uint16_t *w;  // weights, n x ldw, plane stride pw (elements)
+  const uint16_t *x;  // activations, rows x ldx, plane stride px
+  const float *bias, *bn_scale, *bn_offset;
+  float *y32;         // fp32 output (ldy floats per row), or
+  uint16_t *y16;      // split output (ldy elements per row, plane stride py)
+  int ldw, pw, ldx, px, ldy, py;
+  int m, n, kpad, din;
+  uint64_t off_packed;  // splice offset of segment s in signed byte s
+  int post[4];
+  int npost, post_mode;
+  int tiles_m, tiles_n, group;
+};
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void glds16(const char *src, char *lds_dst) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                   (__attribute__((address_space(3))) void *)lds_dst, 16, 0, 0);
+}
+
+__device__ __forceinline__ uint16_t bf16_bits(__bf16 b) { return __builtin_bit_cast(uint16_t, b); }
+
+// v = h + m + l in bf16 (round-to-nearest-even at each step, v_cvt_pk_bf16_f32)
+__device__ __forceinline__ void split3(float v, uint16_t *h, uint16_t *m, uint16_t *l) {
+  const __bf16 b0 = (__bf16)v;
+  const float r1 = v - (float)b0;
+  const __bf16 b1 = (__bf16)r1;
+  const float r2 = r1 - (float)b1;
+  *h = bf16_bits(b0);
+  *m = bf16_bits(b1);
+  *l = bf16_bits((__bf16)r2);
+}
+
+template <int BW_, int BF_, int WGW_, int WGF_, int STAGES_>
+struct X6Cfg {
+  static constexpr int BW = BW_, BF = BF_, WGW = WGW_, WGF = WGF_, STAGES = STAGES_;
+  static constexpr int NW = WGW * WGF, NT = 64 * NW;
+  static constexpr int TW = BW / WGW / 16, TF = BF / WGF / 16;  // 16 x 16 fragments per wave
+  static constexpr int QW = 3 * BW / 16, QF = 3 * BF / 16;       // DMA instructions per stage
+  static constexpr int NQW = QW / NW, NQF = QF / NW;
+  static constexpr int STAGE = 3 * (BW + BF) * 64;                // bytes per stage
+  static_assert(TW >= 1 && TF >= 1 && QW % NW == 0 && QF % NW == 0, "bad bf16x6 tile");
+  static_assert(STAGES == 2 || STAGES == 3, "2 or 3 LDS stages");
+  static_assert(STAGES * STAGE <= 160 * 1024, "LDS");
+};
+
+// Epilogue: lane holds units n .. n+3 of frame f for each fragment pair.
+// + bias, post chain in model order with the reference's roundings; an
+// absent bias adds -0 (identity).  Requires n % 4 == 0 (host-checked).
+template <int TW, int TF, bool OUT16>
+__device__ __forceinline__ void x6_epilogue(const X6Args &p, const f32x4 (&acc)[TW][TF], int nw0, int fw0, int lane) {
+  with_post_mode(p.post_mode, [&](auto M) {
+#pragma unroll
+    for (int i = 0; i < TW; ++i) {
+      const int n = nw0 + i * 16 + 4 * (lane >> 4);
+      if (n >= p.n) continue;
+      const f32x4 bias = p.bias ? *reinterpret_cast<const f32x4 *>(p.bias + n) : f32x4{-0.0f, -0.0f, -0.0f, -0.0f};
+      const f32x4 sc = p.bn_scale ? *reinterpret_cast<const f32x4 *>(p.bn_scale + n) : f32x4{1.0f, 1.0f, 1.0f, 1.0f};
+      const f32x4 of = p.bn_offset ? *reinterpret_cast<const f32x4 *>(p.bn_offset + n) : f32x4{-0.0f, -0.0f, -0.0f, -0.0f};
+#pragma unroll
+      for (int j = 0; j < TF; ++j) {
+        const int f = fw0 + j * 16 + (lane & 15);
+        if (f >= p.m) continue;
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = apply_post<decltype(M)::value>(acc[i][j][e] + bias[e], sc[e], of[e], p.post, p.npost);
+        if constexpr (OUT16) {
+          uint16_t h[4], m[4], l[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) split3(v[e], &h[e], &m[e], &l[e]);
+          uint16_t *dst = p.y16 + (int64_t)f * p.ldy + n;
+          typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
+          *reinterpret_cast<u16x4 *>(dst) = u16x4{h[0], h[1], h[2], h[3]};
+          *reinterpret_cast<u16x4 *>(dst + p.py) = u16x4{m[0], m[1], m[2], m[3]};
+          *reinterpret_cast<u16x4 *>(dst + 2 * p.py) = u16x4{l[0], l[1], l[2], l[3]};
+        } else {
+          *reinterpret_cast<f32x4 *>(p.y32 + (int64_t)f * p.ldy + n) = v;
+        }
+      }
+    }
+  });
+}
+
+// DIAG (tuning builds only, wrong results): 1 = DMAs and fragment reads
+// without the MFMAs, 2 = fragment reads and MFMAs without the DMAs.
+template <class C, bool OUT16, int DIAG = 0>
+__global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6_kernel(X6Args p) {
+  constexpr int BW = C::BW, BF = C::BF, TW = C::TW, TF = C::TF;
+  constexpr int NQW = C::NQW, NQF = C::NQF, STAGES = C::STAGES, STAGE = C::STAGE;
+  __shared__ __attribute__((aligned(1024))) char smem[STAGES * STAGE];
+  auto swz = [](int row) { return ((row >> 3) & 1) << 1; };
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ww = wave / C::WGF, wf = wave % C::WGF;
+  int tm, tn;
+  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
+  if (DIAG == 4) tm = tn = 0;  // every block loads tile (0, 0): L2-resident operands
+  const int f0 = tm * BF, n0 = tn * BW;
+
+  // DMA lane geometry: lane -> (row lane/4 of the instruction's 16, chunk lane%4)
+  // DIAG 3/4: the same bytes fetched as 8 rows x 128 B per instruction
+  constexpr bool FULL = DIAG == 3 || DIAG == 4;
+  const int lrow = FULL ? lane >> 3 : lane >> 2, lch = FULL ? lane & 7 : lane & 3;
+  constexpr int RPQ = FULL ? 8 : 16;
+  uint32_t woff[NQW];
+#pragma unroll
+  for (int i = 0; i < NQW; ++i) {
+    const int q = wave * NQW + i, plane = q / (BW / 16), row = (q % (BW / 16)) * RPQ + lrow;
+    woff[i] = (uint32_t)((min(n0 + row, p.n - 1) * p.ldw + plane * p.pw + 8 * (lch ^ swz(row))) * 2);
+  }
+  uint32_t xoff[NQF];
+  int cur_seg = -1;
+
+  auto issue = [&](int kt) {
+    const int k0 = FULL ? min(kt * 32, p.kpad - 64) : kt * 32;
+    const int seg = k0 / p.din, col0 = k0 - seg * p.din;
+    if (seg != cur_seg) {
+      cur_seg = seg;
+      const int shift = (int)(signed char)(p.off_packed >> (8 * seg));
+#pragma unroll
+      for (int i = 0; i < NQF; ++i) {
+        const int q = wave * NQF + i, plane = q / (BF / 16), row = (q % (BF / 16)) * RPQ + lrow;
+        const int src = clampi(f0 + row + shift, 0, p.m - 1);
+        xoff[i] = (uint32_t)((src * p.ldx + plane * p.px + 8 * (lch ^ swz(row))) * 2);
+      }
+    }
+    char *st = smem + (kt % STAGES) * STAGE;
+    const char *wbase = reinterpret_cast<const char *>(p.w) + (size_t)k0 * 2;
+    const char *xbase = reinterpret_cast<const char *>(p.x) + (size_t)col0 * 2;
+#pragma unroll
+    for (int i = 0; i < NQW; ++i) glds16(wbase + woff[i], st + (wave * NQW + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < NQF; ++i) glds16(xbase + xoff[i], st + 3 * BW * 64 + (wave * NQF + i) * 1024);
+  };
+
+  // fragment read: lane reads row (lane & 15) of the 16-row fragment, logical
+  // chunk lane >> 4 (k = 8 (lane >> 4) .. +7), stored at chunk ^ swz(row)
+  const int foff = (lane & 15) * 64 + (((lane >> 4) ^ (((lane >> 3) & 1) << 1)) * 16);
+  const int wrow = ww * TW * 16, frow = wf * TF * 16;
+
+  f32x4 acc[TW][TF];
+#pragma unroll
+  for (int i = 0; i < TW; ++i)
+#pragma unroll
+    for (int j = 0; j < TF; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+
+  const int ktiles = p.kpad / 32;
+  if (DIAG != 2) issue(0);
+  if (DIAG != 2 && STAGES == 3 && ktiles > 1) issue(1);
+  for (int kt = 0; kt < ktiles; ++kt) {
+    if (DIAG != 2 && STAGES == 3 && kt + 1 < ktiles)
+      wait_vmcnt<NQW + NQF>();  // leave tile kt+1's DMAs in flight
+    else
+      wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (DIAG != 2 && kt + STAGES - 1 < ktiles) issue(kt + STAGES - 1);
+    const char *st = smem + (kt % STAGES) * STAGE;
+    bf16x8 a[3][TW], b[3][TF];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+      for (int i = 0; i < TW; ++i)
+        a[pl][i] = *reinterpret_cast<const bf16x8 *>(st + (pl * BW + wrow + i * 16) * 64 + foff);
+#pragma unroll
+      for (int j = 0; j < TF; ++j)
+        b[pl][j] = *reinterpret_cast<const bf16x8 *>(st + 3 * BW * 64 + (pl * BF + frow + j * 16) * 64 + foff);
+    }
+    if constexpr (DIAG == 1 || DIAG == 3 || DIAG == 4) {
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      u32x4 x = {0, 0, 0, 0};
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+        for (int i = 0; i < TW; ++i) x ^= __builtin_bit_cast(u32x4, a[pl][i]);
+#pragma unroll
+        for (int j = 0; j < TF; ++j) x ^= __builtin_bit_cast(u32x4, b[pl][j]);
+      }
+      acc[0][0][0] += (float)((x[0] ^ x[1] ^ x[2] ^ x[3]) & 1u);
+      continue;
+    }
+#pragma unroll
+    for (int i = 0; i < TW; ++i)
+#pragma unroll
+      for (int j = 0; j < TF; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < TW; ++i)
+#pragma unroll
+      for (int j = 0; j < TF; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[1][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[0][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[1][j], acc[i][j], 0, 0, 0);
+      }
+#pragma unroll
+    for (int i = 0; i < TW; ++i)
+#pragma unroll
+      for (int j = 0; j < TF; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[2][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2][i], b[0][j], acc[i][j], 0, 0, 0);
+      }
+  }
+
+  x6_epilogue<TW, TF, OUT16>(p, acc, n0 + wrow, f0 + frow, lane);
+}
+
+// Phased schedule (3 LDS stages): each K-tile's MFMAs run in three groups
+// by the plane they first need -- w0x0 | w0x1 w1x0 w1x1 | w0x2 w2x0 -- and
+// the fragment reads of the next plane are issued before each group, so LDS
+// latency hides under MFMAs.  The one barrier per K-tile sits before the last
+// group; after it the DMAs of tile kt+2 are issued and tile kt+1's plane-0
+// fragments are read (into the other of two plane-0 register sets) under
+// that group.
+//   WAR: tile kt+2 goes to stage (kt-1) % 3, whose every read fed an MFMA
+//   that each wave issued before this barrier.
+//   RAW: tile kt+1 is read only after the barrier that follows every wave's
+//   vmcnt(0) -- its DMAs, issued one tile earlier, are the only ones
+//   outstanding there.
+template <class C, bool OUT16, bool PRIO>
+__global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6p_kernel(X6Args p) {
+  constexpr int BW = C::BW, BF = C::BF, TW = C::TW, TF = C::TF;
+  constexpr int NQW = C::NQW, NQF = C::NQF, STAGE = C::STAGE;
+  static_assert(C::STAGES == 3, "the phased schedule needs three LDS stages");
+  __shared__ __attribute__((aligned(1024))) char smem[3 * STAGE];
+  auto swz = [](int row) { return ((row >> 3) & 1) << 1; };
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ww = wave / C::WGF, wf = wave % C::WGF;
+  int tm, tn;
+  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
+  const int f0 = tm * BF, n0 = tn * BW;
+
+  const int lrow = lane >> 2, lch = lane & 3;
+  uint32_t woff[NQW];
+#pragma unroll
+  for (int i = 0; i < NQW; ++i) {
+    const int q = wave * NQW + i, plane = q / (BW / 16), row = (q % (BW / 16)) * 16 + lrow;
+    woff[i] = (uint32_t)((min(n0 + row, p.n - 1) * p.ldw + plane * p.pw + 8 * (lch ^ swz(row))) * 2);
+  }
+  uint32_t xoff[NQF];
+  int cur_seg = -1;
+  auto issue = [&](int kt) {
+    const int k0 = kt * 32;
+    const int seg = k0 / p.din, col0 = k0 - seg * p.din;
+    if (seg != cur_seg) {
+      cur_seg = seg;
+      const int shift = (int)(signed char)(p.off_packed >> (8 * seg));
+#pragma unroll
+      for (int i = 0; i < NQF; ++i) {
+        const int q = wave * NQF + i, plane = q / (BF / 16), row = (q % (BF / 16)) * 16 + lrow;
+        const int src = clampi(f0 + row + shift, 0, p.m - 1);
+        xoff[i] = (uint32_t)((src * p.ldx + plane * p.px + 8 * (lch ^ swz(row))) * 2);
+      }
+    }
+    char *st = smem + (kt % 3) * STAGE;
+    const char *wbase = reinterpret_cast<const char *>(p.w) + (size_t)k0 * 2;
+    const char *xbase = reinterpret_cast<const char *>(p.x) + (size_t)col0 * 2;
+#pragma unroll
+    for (int i = 0; i < NQW; ++i) glds16(wbase + woff[i], st + (wave * NQW + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < NQF; ++i) glds16(xbase + xoff[i], st + 3 * BW * 64 + (wave * NQF + i) * 1024);
+  };
+
+  const int foff = (lane & 15) * 64 + (((lane >> 4) ^ (((lane >> 3) & 1) << 1)) * 16);
+  const int wrow = ww * TW * 16, frow = wf * TF * 16;
+  auto rd = [&](const char *st, int pl, bf16x8 *a, bf16x8 *b) {
+#pragma unroll
+    for (int i = 0; i < TW; ++i) a[i] = *reinterpret_cast<const bf16x8 *>(st + (pl * BW + wrow + i * 16) * 64 + foff);
+#pragma unroll
+    for (int j = 0; j < TF; ++j)
+      b[j] = *reinterpret_cast<const bf16x8 *>(st + 3 * BW * 64 + (pl * BF + frow + j * 16) * 64 + foff);
+  };
+  f32x4 acc[TW][TF];
+#pragma unroll
+  for (int i = 0; i < TW; ++i)
+#pragma unroll
+    for (int j = 0; j < TF; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  auto mm = [&](const bf16x8 *a, const bf16x8 *b) {
+#pragma unroll
+    for (int i = 0; i < TW; ++i)
+#pragma unroll
+      for (int j = 0; j < TF; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+  };
+
+  const int ktiles = p.kpad / 32;
+  bf16x8 a0[2][TW], b0[2][TF], a1[TW], b1[TF], a2[TW], b2[TF];
+  issue(0);
+  wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
+  if (ktiles > 1) issue(1);
+  rd(smem, 0, a0[0], b0[0]);
+
+  auto body = [&](int kt, auto cc) {
+    constexpr int c = decltype(cc)::value;
+    const char *st = smem + (kt % 3) * STAGE;
+    rd(st, 1, a1, b1);
+    if (PRIO) __builtin_amdgcn_s_setprio(1);
+    mm(a0[c], b0[c]);
+    rd(st, 2, a2, b2);
+    mm(a0[c], b1);
+    mm(a1, b0[c]);
+    mm(a1, b1);
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
+    if (kt + 1 < ktiles) {
+      wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      if (kt + 2 < ktiles) issue(kt + 2);
+      rd(smem + ((kt + 1) % 3) * STAGE, 0, a0[c ^ 1], b0[c ^ 1]);
+    }
+    if (PRIO) __builtin_amdgcn_s_setprio(1);
+    mm(a0[c], b2);
+    mm(a2, b0[c]);
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
+  };
+  for (int kt = 0; kt < ktiles; kt += 2) {
+    body(kt, std::integral_constant<int, 0>());
+    if (kt + 1 < ktiles) body(kt + 1, std::integral_constant<int, 1>());
+  }
+
+  x6_epilogue<TW, TF, OUT16>(p, acc, n0 + wrow, f0 + frow, lane);
+}
+
+// First layer: the spliced, zero-padded block (splice_pad_kernel's output)
+// written directly as three bf16 planes.  out row r = [plane0 | plane1 |
+// plane2], each `po` wide; columns nseg*din .. po-1 are zero.
+struct SpliceIdx8 {
+  int v[8];
+};
+
+__global__ __launch_bounds__(256) void splice_pad_split_kernel(const float *__restrict__ in, int ld_in, int rows,
+                                                               int din, int nseg, SpliceIdx8 idx,
+                                                               const int *__restrict__ row_map,
+                                                               uint16_t *__restrict__ out, int po) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  uint16_t *o = out + (int64_t)r * 3 * po;
+  for (int c = lane; c < po; c += 64) {
+    const int s = c / din;
+    float v = 0.0f;
+    if (s < nseg) {
+      int src = clampi(r + idx.v[s], 0, rows - 1);
+      if (row_map) src = row_map[src];
+      v = in[(int64_t)src * ld_in + (c - s * din)];
+    }
+    uint16_t h, m, l;
+    split3(v, &h, &m, &l);
+    o[c] = h;
+    o[po + c] = m;
+    o[2 * po + c] = l;
+  }
+}
+
+template <class C, int DIAG = 0>
+int launch_cfg(hipStream_t s, X6Args p, bool out16) {
+  p.tiles_n = (p.n + C::BW - 1) / C::BW;
+  p.tiles_m = (p.m + C::BF - 1) / C::BF;
+  dim3 grid(p.tiles_m * p.tiles_n), block(C::NT);
+  if (out16)
+    hipLaunchKernelGGL((gemm_bf16x6_kernel<C, true, DIAG>), grid, block, 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_bf16x6_kernel<C, false, DIAG>), grid, block, 0, s, p);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
+template <class C, bool PRIO = false>
+int launch_phased(hipStream_t s, X6Args p, bool out16) {
+  p.tiles_n = (p.n + C::BW - 1) / C::BW;
+  p.tiles_m = (p.m + C::BF - 1) / C::BF;
+  dim3 grid(p.tiles_m * p.tiles_n), block(C::NT);
+  if (out16)
+    hipLaunchKernelGGL((gemm_bf16x6p_kernel<C, true, PRIO>), grid, block, 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_bf16x6p_kernel<C, false, PRIO>), grid, block, 0, s, p);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
+int x6_variant() {
+  static int v = [] {
+    const char *e = getenv("CATEARS_X6_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+}  // namespace
+
+int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
+  if (a.m <= 0 || a.n <= 0) return CE_GPU_OK;
+  if (a.kpad % 32 != 0 || a.din % 32 != 0 || a.nseg < 1 || a.nseg > 8 || a.nseg * a.din > a.kpad)
+    return fail(CE_GPU_EINVAL, "gemm_bf16x6: bad K geometry");
+  if (a.n % 4 != 0 || a.ldy % 4 != 0 || (a.y16 && a.py % 4 != 0))
+    return fail(CE_GPU_EINVAL, "gemm_bf16x6: output width must be a multiple of 4");
+  if (a.ldw % 8 || a.pw % 8 || a.ldx % 8 || a.px % 8 || (reinterpret_cast<uintptr_t>(a.w) & 15) ||
+      (reinterpret_cast<uintptr_t>(a.x) & 15))
+    return fail(CE_GPU_EINVAL, "gemm_bf16x6: operands must be 16-byte aligned");
+  if ((int64_t)a.n * a.ldw * 2 >= ((int64_t)1 << 32) || (int64_t)a.m * a.ldx * 2 >= ((int64_t)1 << 32))
+    return fail(CE_GPU_EINVAL, "gemm_bf16x6: operand beyond 4 GiB");
+  if (a.npost > 4) return fail(CE_GPU_EINVAL, "gemm_bf16x6: too many post ops");
+  X6Args p;
+  p.w = a.w;
+  p.x = a.x;
+  p.bias = a.bias;
+  p.bn_scale = a.bn_scale;
+  p.bn_offset = a.bn_offset;
+  p.y32 = a.y32;
+  p.y16 = a.y16;
+  p.ldw = a.ldw;
+  p.pw = a.pw;
+  p.ldx = a.ldx;
+  p.px = a.px;
+  p.ldy = a.ldy;
+  p.py = a.py;
+  p.m = a.m;
+  p.n = a.n;
+  p.kpad = a.kpad;
+  p.din = a.din;
+  p.off_packed = 0;
+  for (int i = 0; i < a.nseg; ++i) {
+    if (a.off[i] < -128 || a.off[i] > 127) return fail(CE_GPU_ENOTSUP, "gemm_bf16x6: splice offset beyond +-127");
+    p.off_packed |= (uint64_t)(uint8_t)(int8_t)a.off[i] << (8 * i);
+  }
+  for (int i = 0; i < 4; ++i) p.post[i] = a.post[i];
+  p.npost = a.npost;
+  p.post_mode = post_mode(a.post, a.npost);
+  p.group = 8;
+  const bool out16 = a.y16 != nullptr;
+  switch (x6_variant()) {
+    case 1:
+      return launch_cfg<X6Cfg<128, 128, 2, 2, 3>>(s, p, out16);
+    case 2:
+      return launch_cfg<X6Cfg<64, 128, 2, 2, 2>>(s, p, out16);
+    case 3:
+      return launch_cfg<X6Cfg<128, 64, 2, 2, 2>>(s, p, out16);
+    case 4:
+      return launch_cfg<X6Cfg<64, 128, 2, 2, 3>>(s, p, out16);
+    case 5:
+      return launch_cfg<X6Cfg<128, 64, 2, 2, 3>>(s, p, out16);
+    case 6:
+      return launch_phased<X6Cfg<128, 128, 2, 2, 3>>(s, p, out16);
+    case 7:
+      return launch_phased<X6Cfg<128, 128, 2, 4, 3>>(s, p, out16);
+    case 8:
+      return launch_phased<X6Cfg<128, 128, 4, 2, 3>>(s, p, out16);
+    case 9:
+      return launch_cfg<X6Cfg<128, 128, 2, 4, 2>>(s, p, out16);
+    case 10:
+      return launch_phased<X6Cfg<128, 128, 2, 4, 3>, true>(s, p, out16);
+    case 11:
+      return launch_phased<X6Cfg<128, 128, 2, 2, 3>, true>(s, p, out16);
+    case 12:
+      return launch_phased<X6Cfg<64, 128, 2, 2, 3>>(s, p, out16);
+    case 93:
+      return launch_cfg<X6Cfg<128, 128, 2, 4, 3>>(s, p, out16);
+    case 94:  // tuning only
+      return launch_cfg<X6Cfg<128, 128, 2, 4, 3>, 1>(s, p, out16);
+    case 95:
+      return launch_cfg<X6Cfg<256, 128, 4, 2, 2>>(s, p, out16);
+    case 96:  // tuning only
+      return launch_cfg<X6Cfg<256, 128, 4, 2, 2>, 1>(s, p, out16);
+    case 97:
+      return launch_cfg<X6Cfg<128, 256, 2, 4, 2>>(s, p, out16);
+    case 98:  // tuning only
+      return launch_cfg<X6Cfg<128, 256, 2, 4, 2>, 1>(s, p, out16);
+    case 99:  // tuning only: DMAs as 8 rows x 128 B + fragment reads, no MFMA (wrong results)
+      return launch_cfg<X6Cfg<128, 128, 2, 4, 2>, 3>(s, p, out16);
+    case 100:  // tuning only: as 99 with three stages
+      return launch_cfg<X6Cfg<128, 128, 2, 4, 3>, 3>(s, p, out16);
+    case 101:  // tuning only: as 99, every block on tile (0, 0)
+      return launch_cfg<X6Cfg<128, 128, 2, 4, 2>, 4>(s, p, out16);
+    case 102:  // tuning only: as 100, every block on tile (0, 0)
+      return launch_cfg<X6Cfg<128, 128, 2, 4, 3>, 4>(s, p, out16);
+    case 91:  // tuning only: DMAs + fragment reads, no MFMA (wrong results)
+      return launch_cfg<X6Cfg<128, 128, 2, 4, 2>, 1>(s, p, out16);
+    case 92:  // tuning only: fragment reads + MFMA, no DMA (wrong results)
+      return launch_cfg<X6Cfg<128, 128, 2, 4, 2>, 2>(s, p, out16);
+    default:
+      return launch_cfg<X6Cfg<128, 128, 2, 2, 2>>(s, p, out16);
+  }
+}
+
+int launch_splice_pad_split(hipStream_t s, const float *in, int ld_in, int rows, int din, int nseg, const int *off,
+                            const int *row_map, uint16_t *out, int po) {
+  if (nseg < 1 || nseg > 8 || nseg * din > po) return fail(CE_GPU_EINVAL, "splice_pad_split: bad geometry");
+  SpliceIdx8 idx = {};
+  for (int i = 0; i < nseg; ++i) idx.v[i] = off[i];
+  if (rows > 0)
+    hipLaunchKernelGGL(splice_pad_split_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, in, ld_in, rows, din, nseg,
+                       idx, row_map, out, po);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
+}  // namespace catears

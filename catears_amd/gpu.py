@@ -30,7 +30,11 @@ ABI = [
     "ce_gpu_nnet_propagate", "ce_gpu_linear", "ce_gpu_splice", "ce_gpu_rowwise",
     "ce_gpu_profile_anchor", "ce_gpu_ctx_profile_intervals", "ce_gpu_model_quantize",
     "ce_gpu_nnet_propagate_blocks", "ce_gpu_loglik_gather", "ce_gpu_loglik_columns",
+    "ce_gpu_model_set_gemm", "ce_gpu_model_get_gemm", "ce_gpu_ctx_overflow",
 ]
+
+# ce_gpu_model_set_gemm modes
+GEMM_MODES = {"fp32": 0, "bf16x6": 1, "f16x3": 2}
 
 _lib = None
 
@@ -90,6 +94,9 @@ def lib():
         "ce_gpu_rowwise": (ci, [vp, ci, ci, ci, vp, ci, vp, vp]),
         "ce_gpu_loglik_gather": (ci, [vp, vp, ci, ci, vp, ci, vp, vp, ci, ctypes.c_float, vp]),
         "ce_gpu_loglik_columns": (ci, [vp, vp, ci, ci, ci, vp, ci, vp]),
+        "ce_gpu_model_set_gemm": (ci, [vp, ci]),
+        "ce_gpu_model_get_gemm": (ci, [vp, pi]),
+        "ce_gpu_ctx_overflow": (ci, [vp, pi]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -132,6 +139,13 @@ class Context:
 
     def synchronize(self):
         check(lib().ce_gpu_ctx_synchronize(self.h))
+
+    def overflow(self):
+        """True if an f16x3 GEMM met an out-of-range activation since the
+        last call (synchronizes; ce_gpu_ctx_overflow)."""
+        v = ctypes.c_int()
+        check(lib().ce_gpu_ctx_overflow(self.h, ctypes.byref(v)))
+        return bool(v.value)
 
     PROF_GEMM, PROF_GEMM_GATHER, PROF_FBANK, PROF_CMVN, PROF_FINALIZE, PROF_QUANT = range(6)
 
@@ -197,6 +211,19 @@ class Model:
         """Switch to the int8 path (ce_gpu_model_quantize)."""
         check(lib().ce_gpu_model_quantize(ctx.h, self.h))
         return self
+
+    def set_gemm(self, mode):
+        """Matrix-core form of the fp32 Linear layers: "fp32" (fp32 MFMA),
+        "bf16x6" (three-plane bf16 split, six products) or "f16x3" (two scaled
+        fp16 planes, three products); ce_gpu_model_set_gemm."""
+        check(lib().ce_gpu_model_set_gemm(self.h, GEMM_MODES[mode]))
+        return self
+
+    @property
+    def gemm(self):
+        v = ctypes.c_int()
+        check(lib().ce_gpu_model_get_gemm(self.h, ctypes.byref(v)))
+        return {b: a for a, b in GEMM_MODES.items()}[v.value]
 
     def tid2pdf(self):
         n = ctypes.c_int()

@@ -71,6 +71,11 @@ int ce_gpu_ctx_destroy(ce_gpu_ctx *ctx);
 int ce_gpu_ctx_set_stream(ce_gpu_ctx *ctx, void *stream);
 /* Block the host until all work enqueued through ctx has finished. */
 int ce_gpu_ctx_synchronize(ce_gpu_ctx *ctx);
+/* Synchronizes ctx's stream, returns in *overflow whether an f16x3 GEMM
+ * (CE_GPU_GEMM_F16X3) met an activation outside its range since the last
+ * call, and clears the word.  When set, the log-likelihoods computed through
+ * ctx since the last call are not fp32-accurate. */
+int ce_gpu_ctx_overflow(ce_gpu_ctx *ctx, int *overflow);
 
 /* Kernel timing for roofline reporting: while enabled, every launch of the
  * given kernel class is bracketed by a pair of HIP events on the context's
@@ -127,6 +132,35 @@ int ce_gpu_model_info(const ce_gpu_model *m, int *left_context, int *right_conte
  * accumulation is exact (gemmlowp's ring), bias / ReLU / BatchNorm /
  * LogSoftmax stay fp32.  Irreversible for this model handle. */
 int ce_gpu_model_quantize(ce_gpu_ctx *ctx, ce_gpu_model *m);
+
+/* Matrix-core form of the fp32 Linear layers (LinearLayer::Propagate ->
+ * MatMat -> cblas_sgemm, src/nnet.cc:22-36, src/matrix.cc:300-323):
+ *   CE_GPU_GEMM_FP32   v_mfma_f32_32x32x2_f32 (exact fp32 products)
+ *   CE_GPU_GEMM_BF16X6 every fp32 operand split exactly into three bf16
+ *                      planes, six bf16 MFMA products per pair accumulated in
+ *                      fp32; the dropped cross terms are < 2^-25 |w x|, below
+ *                      one fp32 rounding, so the result is an fp32 GEMM
+ *                      (differently ordered sum), on the 16x faster bf16
+ *                      matrix cores.
+ *   CE_GPU_GEMM_F16X3  every operand, scaled by a power of two, as two fp16
+ *                      planes (22-23 significant bits), three fp16 MFMA
+ *                      products in two fp32 accumulators; dropped term
+ *                      < 2^-22 |w x|.  Log-likelihood error measured equal to
+ *                      the FP32 path's.  Hidden activations must stay below
+ *                      1.6e7 in magnitude (and finite): otherwise the
+ *                      context's overflow word is set (ce_gpu_ctx_overflow)
+ *                      and those results must be recomputed in another mode.
+ * Models load in CE_GPU_GEMM_F16X3 when their program allows it (every
+ * Linear's input width after the first a multiple of 32, output widths
+ * multiples of 4, every ReLU/BatchNorm fused into a Linear, finite weights),
+ * else BF16X6 / FP32; environment CATEARS_NNET_GEMM=fp32|bf16x6|f16x3
+ * overrides the default.  Setting a mode the model does not allow returns
+ * CE_GPU_ENOTSUP. */
+#define CE_GPU_GEMM_FP32 0
+#define CE_GPU_GEMM_BF16X6 1
+#define CE_GPU_GEMM_F16X3 2
+int ce_gpu_model_set_gemm(ce_gpu_model *m, int mode);
+int ce_gpu_model_get_gemm(const ce_gpu_model *m, int *mode);
 
 /* tid2pdf map (AcousticModel::TransitionPdfIdMap, src/am.h:38-40).  Copies
  * min(capacity, size) ints to h_out and returns the size via *size. */

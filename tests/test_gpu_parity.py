@@ -145,10 +145,11 @@ def am_oracle(oracle, am, feats, gemm=None):
     return oracle.am_stream(am, feats, chunk_size=am["chunk"], gemm=gemm)
 
 
-def test_am_xs_vs_oracle(torch, G, ctx, oracle, xs_config):
+@pytest.mark.parametrize("gemm", ["fp32", "bf16x6", "f16x3"])
+def test_am_xs_vs_oracle(torch, G, ctx, oracle, xs_config, gemm):
     from catears_amd import formats, synth
     am = formats.read_am(xs_config)
-    model = G.Model(ctx, xs_config)
+    model = G.Model(ctx, xs_config).set_gemm(gemm)
     assert (model.left, model.right, model.input_dim, model.num_pdfs) == (10, 10, 40, 512)
     assert np.array_equal(model.tid2pdf(), am["tid2pdf"])
     fb = oracle.Fbank()
@@ -167,12 +168,13 @@ def test_am_xs_vs_oracle(torch, G, ctx, oracle, xs_config):
             assert np.abs(o[off[u]:off[u + 1]] - ref).max() <= LOGLIK_TOL, f"utt {u}"
 
 
-def test_am_segmentation_is_exact(torch, G, ctx, oracle, xs_config):
+@pytest.mark.parametrize("gemm", ["fp32", "bf16x6", "f16x3"])
+def test_am_segmentation_is_exact(torch, G, ctx, oracle, xs_config, gemm):
     """Splitting an utterance over chunks (max_rows) must not change a bit:
     every output element is the same k-ordered MFMA chain whatever the row's
     position."""
     from catears_amd import synth
-    model = G.Model(ctx, xs_config)
+    model = G.Model(ctx, xs_config).set_gemm(gemm)
     fb = oracle.Fbank()
     feats = [fb.compute(synth.pcm(400 + i, n)) for i, n in enumerate([48000, 16000, 30000])]
     ns = [(len(x) - 1) * 160 + 400 for x in feats]
@@ -185,13 +187,14 @@ def test_am_segmentation_is_exact(torch, G, ctx, oracle, xs_config):
     assert np.array_equal(bits(outs[0]), bits(outs[2]))
 
 
-def test_am_s_vs_oracle(torch, G, ctx, oracle, s_config):
+@pytest.mark.parametrize("gemm", ["fp32", "bf16x6", "f16x3"])
+def test_am_s_vs_oracle(torch, G, ctx, oracle, s_config, gemm):
     """Benchmark model (TDNN-S, 34.75 MFLOP/frame) on two utterances; the
     oracle's GEMM is numpy fp32 here for speed (any fp32 summation order is
     the reference algorithm; OpenBLAS's order is not pinned either)."""
     from catears_amd import formats, synth
     am = formats.read_am(s_config)
-    model = G.Model(ctx, s_config)
+    model = G.Model(ctx, s_config).set_gemm(gemm)
     assert model.num_pdfs == 3456 and model.num_linear == 7
     fb = oracle.Fbank()
     feats = [fb.compute(synth.pcm(500 + i, n)) for i, n in enumerate([48000, 20000])]
@@ -201,6 +204,34 @@ def test_am_s_vs_oracle(torch, G, ctx, oracle, s_config):
     for u, x in enumerate(feats):
         ref = oracle.am_whole(am, x, gemm=lambda a, w: a @ w)
         assert np.abs(out[off[u]:off[u + 1]] - ref).max() <= LOGLIK_TOL
+
+
+def test_split_gemms_are_fp32_accurate(torch, G, ctx, oracle, s_config):
+    """The bf16x6 and f16x3 split GEMMs are fp32 GEMMs: on TDNN-S their
+    log-likelihood error against an fp64 evaluation of the same network is of
+    the fp32-MFMA path's size, and far inside 1e-4.  A single-plane bf16 or
+    fp16 GEMM would miss by orders of magnitude."""
+    from catears_amd import formats, synth
+    am = formats.read_am(s_config)
+    fb = oracle.Fbank()
+    feats = [fb.compute(synth.pcm(520 + i, n)) for i, n in enumerate([64000, 32000])]
+    x = dev(torch, np.concatenate(feats))
+    errs = {}
+    for gemm in ("fp32", "bf16x6", "f16x3"):
+        model = G.Model(ctx, s_config).set_gemm(gemm)
+        assert model.gemm == gemm
+        plan = G.Plan(ctx, [64000, 32000], model)
+        out = G.am_forward(ctx, model, plan, x).cpu().numpy()
+        off = plan.frame_offsets
+        e = 0.0
+        for u, f in enumerate(feats):
+            ref = oracle.am_whole(am, f, gemm=lambda a, w: (a.astype(np.float64) @ w.astype(np.float64)).astype(np.float32))
+            e = max(e, float(np.abs(out[off[u]:off[u + 1]] - ref).max()))
+        errs[gemm] = e
+    for gemm in ("bf16x6", "f16x3"):
+        assert errs[gemm] <= max(2.0 * errs["fp32"], 2e-5), errs
+        assert errs[gemm] <= LOGLIK_TOL / 2, errs
+    assert not ctx.overflow()
 
 
 def test_score_pipeline_with_cmvn(torch, G, ctx, oracle, xs_config, global_stats):
@@ -276,3 +307,19 @@ def test_quantize_and_u8_gemm_bitexact(torch, G, ctx, oracle, shape):
     assert np.array_equal(got_i, ref_i)
     got_f = G.gemm_u8(ctx, qa, pa, qb, pb).cpu().numpy()
     assert np.array_equal(bits(got_f), bits(oracle.gemm_u8u8f32(oa, sa, za, ob, sb, zb)))
+
+
+def test_f16x3_overflow_is_flagged(torch, G, ctx, xs_config):
+    """Activations beyond the f16x3 range (|x| >= 1.6e7) cannot be stored in
+    the two fp16 planes: the context's overflow word reports it; in range,
+    it stays clear."""
+    model = G.Model(ctx, xs_config).set_gemm("f16x3")
+    rng = np.random.default_rng(7)
+    x = rng.standard_normal((64, 40)).astype(np.float32)
+    assert not ctx.overflow()
+    G.nnet_propagate(ctx, model, dev(torch, x))
+    assert not ctx.overflow()
+    x[10, 3] = 3e7
+    G.nnet_propagate(ctx, model, dev(torch, x))
+    assert ctx.overflow()
+    assert not ctx.overflow()  # read clears it
