@@ -67,7 +67,7 @@ def parse():
                          "frame batch 8192")
     ap.add_argument("--gemm", choices=["fp32", "bf16x6", "f16x3"], default=None,
                     help="matrix-core form of the fp32 Linear layers (ce_gpu_model_set_gemm); default: "
-                         "the library's (f16x3: two scaled fp16 planes, three products, fp32-accurate)")
+                         "the library's (bf16x6: three exact bf16 planes, six products, fp32 GEMM)")
     ap.add_argument("--back-streams", type=int, default=3,
                     help="nnet streams; consecutive batches alternate between them so one batch's "
                          "wave-quantisation tail overlaps the next batch's layers")
@@ -119,7 +119,7 @@ def cpu_baseline(conf, n_utts, seconds, threads, min_wall):
 ROOFLINE_KERNEL = "gemm_f32_glds_kernel<catears::Cfg<128, 64, 32, 2, 2>, 2, false>"
 # split-plane hidden layers (split output), the default variants
 SPLIT_ROOFLINE_KERNEL = {
-    "bf16x6": "gemm_bf16x6_kernel<catears::X6Cfg<128, 128, 2, 4, 2>, true, 0>",
+    "bf16x6": "gemm_bf16x6p_kernel<catears::X6Cfg<128, 128, 2, 4, 3>, true, false>",
     "f16x3": "gemm_f16x3_kernel<catears::X3Cfg<128, 128, 2, 4, 2, 64>, true>",
 }
 SPLIT_DTYPE = {

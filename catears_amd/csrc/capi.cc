@@ -373,7 +373,7 @@ static int default_gemm() {
     if (e && !strcmp(e, "fp32")) return (int)CE_GPU_GEMM_FP32;
     if (e && !strcmp(e, "bf16x6")) return (int)CE_GPU_GEMM_BF16X6;
     if (e && !strcmp(e, "f16x3")) return (int)CE_GPU_GEMM_F16X3;
-    return (int)CE_GPU_GEMM_F16X3;
+    return (int)CE_GPU_GEMM_BF16X6;
   }();
   return g;
 }

@@ -150,12 +150,12 @@ int ce_gpu_model_quantize(ce_gpu_ctx *ctx, ce_gpu_model *m);
  *                      1.6e7 in magnitude (and finite): otherwise the
  *                      context's overflow word is set (ce_gpu_ctx_overflow)
  *                      and those results must be recomputed in another mode.
- * Models load in CE_GPU_GEMM_F16X3 when their program allows it (every
+ * Models load in CE_GPU_GEMM_BF16X6 when their program allows it (every
  * Linear's input width after the first a multiple of 32, output widths
- * multiples of 4, every ReLU/BatchNorm fused into a Linear, finite weights),
- * else BF16X6 / FP32; environment CATEARS_NNET_GEMM=fp32|bf16x6|f16x3
- * overrides the default.  Setting a mode the model does not allow returns
- * CE_GPU_ENOTSUP. */
+ * multiples of 4, every ReLU/BatchNorm fused into a Linear), else FP32.
+ * F16X3 (22-23 significant bits per operand, not a full fp32 significand)
+ * is opt-in.  Environment CATEARS_NNET_GEMM=fp32|bf16x6|f16x3 overrides the
+ * default.  Setting a mode the model does not allow returns CE_GPU_ENOTSUP. */
 #define CE_GPU_GEMM_FP32 0
 #define CE_GPU_GEMM_BF16X6 1
 #define CE_GPU_GEMM_F16X3 2

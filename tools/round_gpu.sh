@@ -19,7 +19,7 @@ echo "bench(rocprof) rc=$rc"; tail -2 "$OUT/bench.log"
 i=0
 for grp in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "gemm_f32|fbank|cmvn|finalize" \
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "gemm_|fbank|cmvn|finalize|splice" \
       --output-format csv -d "$OUT/pmc$i" -o run -- \
       python "$R/bench.py" --steps 4 --warmup 1 --no-cpu-baseline --no-profile --serial \
       > "$OUT/pmc$i.log" 2>&1 || { echo "pmc pass $i failed"; tail -20 "$OUT/pmc$i.log"; exit 1; }
