@@ -100,8 +100,9 @@ struct X6Cfg {
   static constexpr int TW = BW / WGW / 16, TF = BF / WGF / 16;  // 16 x 16 fragments per wave
   static constexpr int QW = 3 * BW / 16, QF = 3 * BF / 16;       // DMA instructions per stage
   static constexpr int NQW = QW / NW, NQF = QF / NW;
+  static constexpr int NQM = (QW + QF) / NW;                      // pieces per wave, mixed
   static constexpr int STAGE = 3 * (BW + BF) * 64;                // bytes per stage
-  static_assert(TW >= 1 && TF >= 1 && QW % NW == 0 && QF % NW == 0, "bad bf16x6 tile");
+  static_assert(TW >= 1 && TF >= 1 && (QW + QF) % NW == 0, "bad bf16x6 tile");
   static_assert(STAGES == 2 || STAGES == 3, "2 or 3 LDS stages");
   static_assert(STAGES * STAGE <= 160 * 1024, "LDS");
 };
@@ -380,6 +381,163 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6p_kernel(X6Args p) {
   x6_epilogue<TW, TF, OUT16>(p, acc, n0 + wrow, f0 + frow, lane);
 }
 
+// Phased schedule, branch-free loop body.  Same three plane groups and LDS
+// ring as gemm_bf16x6p_kernel, but every K-tile step runs the same
+// straight-line code: the barrier, the DMA issue (clamped to the last tile:
+// a dummy refetch into the free stage once the tail is reached) and the next
+// tile's plane-0 fragment reads are unconditional, and the splice row
+// offsets are recomputed per issue (no cached-segment branch).  One basic
+// block per step lets the waitcnt pass count outstanding LDS reads exactly
+// (lgkmcnt(N) instead of the lgkmcnt(0) a control-flow merge forces), so
+// fragment reads of the next group stay in flight under this group's MFMAs.
+// SCHED 1 additionally pins the last group's interleave: two MFMAs per DMA
+// piece / fragment read.
+template <class C, bool OUT16, int SCHED>
+__global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6q_kernel(X6Args p) {
+  constexpr int BW = C::BW, BF = C::BF, TW = C::TW, TF = C::TF;
+  constexpr int STAGE = C::STAGE, NQ = C::NQM, QW = C::QW;
+  static_assert(C::STAGES == 3, "three LDS stages");
+  __shared__ __attribute__((aligned(1024))) char smem[3 * STAGE];
+  auto swz = [](int row) { return ((row >> 3) & 1) << 1; };
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ww = wave / C::WGF, wf = wave % C::WGF;
+  int tm, tn;
+  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
+  const int f0 = tm * BF, n0 = tn * BW;
+
+  // DMA pieces: the stage's QW weight pieces then QF activation pieces (one
+  // piece = 16 rows x 64 B of one plane, stored at stage + 1 KB * piece).
+  // Balanced when both kinds divide over the waves (each wave NQW weight +
+  // NQF activation pieces: measured faster than giving some waves only one
+  // kind); otherwise wave w issues pieces w NQ .. w NQ + NQ - 1 (wave-uniform
+  // selects, no branch).
+  constexpr bool BAL = C::QW % C::NW == 0 && C::QF % C::NW == 0;
+  const int lrow = lane >> 2, lch = lane & 3;
+  bool isw[NQ];
+  int piece[NQ];
+  uint32_t pconst[NQ];  // weight: byte offset at K-tile 0; activation: plane / chunk offset
+  int xrow[NQ];         // activation tile row
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    int q;
+    if constexpr (BAL) {
+      isw[i] = i < C::NQW;
+      q = isw[i] ? wave * C::NQW + i : QW + wave * C::NQF + (i - C::NQW);
+    } else {
+      q = wave * NQ + i;
+      isw[i] = q < QW;
+    }
+    piece[i] = q;
+    if (isw[i]) {
+      const int plane = q / (BW / 16), row = (q % (BW / 16)) * 16 + lrow;
+      pconst[i] = (uint32_t)((min(n0 + row, p.n - 1) * p.ldw + plane * p.pw + 8 * (lch ^ swz(row))) * 2);
+      xrow[i] = 0;
+    } else {
+      const int q2 = q - QW, plane = q2 / (BF / 16), row = (q2 % (BF / 16)) * 16 + lrow;
+      pconst[i] = (uint32_t)((plane * p.px + 8 * (lch ^ swz(row))) * 2);
+      xrow[i] = f0 + row;
+    }
+  }
+  const int ktiles = p.kpad / 32;
+  auto issue = [&](int kt) {
+    kt = min(kt, ktiles - 1);
+    const int k0 = kt * 32;
+    const int seg = k0 / p.din, col0 = k0 - seg * p.din;
+    const int shift = (int)(signed char)(p.off_packed >> (8 * seg));
+    char *st = smem + (kt % 3) * STAGE;
+    const char *wbase = reinterpret_cast<const char *>(p.w) + (size_t)k0 * 2;
+    const char *xbase = reinterpret_cast<const char *>(p.x) + (size_t)col0 * 2;
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+      const uint32_t xo = (uint32_t)(clampi(xrow[i] + shift, 0, p.m - 1) * p.ldx * 2) + pconst[i];
+      const char *src = isw[i] ? wbase + pconst[i] : xbase + xo;
+      glds16(src, st + piece[i] * 1024);
+    }
+  };
+  const int foff = (lane & 15) * 64 + (((lane >> 4) ^ (((lane >> 3) & 1) << 1)) * 16);
+  const int wrow = ww * TW * 16, frow = wf * TF * 16;
+  auto rd = [&](const char *st, int pl, bf16x8 *a, bf16x8 *b) {
+#pragma unroll
+    for (int i = 0; i < TW; ++i) a[i] = *reinterpret_cast<const bf16x8 *>(st + (pl * BW + wrow + i * 16) * 64 + foff);
+#pragma unroll
+    for (int j = 0; j < TF; ++j)
+      b[j] = *reinterpret_cast<const bf16x8 *>(st + 3 * BW * 64 + (pl * BF + frow + j * 16) * 64 + foff);
+  };
+  f32x4 acc[TW][TF];
+#pragma unroll
+  for (int i = 0; i < TW; ++i)
+#pragma unroll
+    for (int j = 0; j < TF; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  auto mm = [&](const bf16x8 *a, const bf16x8 *b) {
+#pragma unroll
+    for (int i = 0; i < TW; ++i)
+#pragma unroll
+      for (int j = 0; j < TF; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+  };
+
+  bf16x8 a0[2][TW], b0[2][TF], a1[TW], b1[TF], a2[TW], b2[TF];
+  issue(0);
+  issue(1);
+  issue(2);
+  wait_vmcnt<2 * NQ>();
+  __builtin_amdgcn_s_barrier();
+  rd(smem, 0, a0[0], b0[0]);
+
+  // Step kt reads stage kt % 3: planes 1 and 2 before its barrier (plane 0
+  // was read at the end of step kt-1), so once every wave has drained its
+  // LDS reads (lgkmcnt(0)) and passed the barrier the stage is free and tile
+  // kt+3 is issued into it -- two steps ahead of its first read.  RAW: tile
+  // kt+1 is read (plane 0) right after the barrier; every wave's vmcnt(NQ)
+  // before it retired all but the newest issue (tile kt+2), i.e. tile kt+1.
+  // In the last steps the issued tile is clamped to ktiles-1: a refetch of
+  // the last tile into the stage it already occupies, writing the bytes it
+  // holds, so any read of that stage sees the same values; it keeps one
+  // issue per step, which the vmcnt count relies on.  The plane-0 read of
+  // the nonexistent tile ktiles is never used.
+  auto body = [&](int kt, auto cc) {
+    constexpr int c = decltype(cc)::value;
+    const char *st = smem + (kt % 3) * STAGE;
+    rd(st, 1, a1, b1);
+    mm(a0[c], b0[c]);
+    rd(st, 2, a2, b2);
+    mm(a0[c], b1);
+    mm(a1, b0[c]);
+    mm(a1, b1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wait_vmcnt<NQ>();
+    __builtin_amdgcn_s_barrier();
+    issue(kt + 3);
+    rd(smem + ((kt + 1) % 3) * STAGE, 0, a0[c ^ 1], b0[c ^ 1]);
+    mm(a0[c], b2);
+    mm(a2, b0[c]);
+    if constexpr (SCHED == 1) {
+      // the last group: 16 MFMAs; interleave the NQ DMA pieces and the
+      // TW + TF plane-0 reads between them
+#pragma unroll
+      for (int g = 0; g < NQ; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read (LDS-DMA)
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      }
+#pragma unroll
+      for (int g = 0; g < TW + TF; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 2 * TW * TF - NQ - TW - TF, 0);
+    }
+  };
+  int kt = 0;
+  for (; kt + 1 < ktiles; kt += 2) {
+    body(kt, std::integral_constant<int, 0>());
+    body(kt + 1, std::integral_constant<int, 1>());
+  }
+  if (kt < ktiles) body(kt, std::integral_constant<int, 0>());
+  wait_vmcnt<0>();  // drain the tail refetches before the block ends
+
+  x6_epilogue<TW, TF, OUT16>(p, acc, n0 + wrow, f0 + frow, lane);
+}
+
 // Register-staged schedule: operands travel global -> VGPR (plain
 // global_load_dwordx4) -> LDS (ds_write_b128) instead of LDS-DMA.  An LDS-DMA
 // piece costs its wave 60-185 issue cycles (MI355X_MICROARCH.md, constants
@@ -562,6 +720,19 @@ int launch_phased(hipStream_t s, X6Args p, bool out16) {
   return CE_GPU_OK;
 }
 
+template <class C, int SCHED>
+int launch_q(hipStream_t s, X6Args p, bool out16) {
+  p.tiles_n = (p.n + C::BW - 1) / C::BW;
+  p.tiles_m = (p.m + C::BF - 1) / C::BF;
+  dim3 grid(p.tiles_m * p.tiles_n), block(C::NT);
+  if (out16)
+    hipLaunchKernelGGL((gemm_bf16x6q_kernel<C, true, SCHED>), grid, block, 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_bf16x6q_kernel<C, false, SCHED>), grid, block, 0, s, p);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
 template <class C>
 int launch_reg(hipStream_t s, X6Args p, bool out16) {
   p.tiles_n = (p.n + C::BW - 1) / C::BW;
@@ -684,10 +855,22 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
       return launch_reg<X6Cfg<256, 128, 4, 2, 2>>(s, p, out16);
     case 18:
       return launch_reg<X6Cfg<64, 128, 2, 2, 2>>(s, p, out16);
+    case 20:
+      return launch_q<X6Cfg<128, 128, 2, 4, 3>, 0>(s, p, out16);
+    case 21:
+      return launch_q<X6Cfg<128, 128, 2, 4, 3>, 1>(s, p, out16);
+    case 22:
+      return launch_q<X6Cfg<128, 128, 4, 2, 3>, 0>(s, p, out16);
+    case 23:
+      return launch_q<X6Cfg<128, 128, 2, 2, 3>, 0>(s, p, out16);
+    case 24:
+      return launch_q<X6Cfg<128, 128, 4, 4, 3>, 0>(s, p, out16);
+    case 25:
+      return launch_q<X6Cfg<128, 128, 8, 2, 3>, 0>(s, p, out16);
     case 13:
       return launch_cfg<X6Cfg<128, 128, 2, 2, 2>>(s, p, out16);
-    default:  // = 7
-      return launch_phased<X6Cfg<128, 128, 2, 4, 3>>(s, p, out16);
+    default:  // = 22
+      return launch_q<X6Cfg<128, 128, 4, 2, 3>, 0>(s, p, out16);
   }
 }
 
