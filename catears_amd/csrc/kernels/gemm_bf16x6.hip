@@ -396,8 +396,8 @@ template <class C, bool OUT16, int SCHED>
 __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6q_kernel(X6Args p) {
   constexpr int BW = C::BW, BF = C::BF, TW = C::TW, TF = C::TF;
   constexpr int STAGE = C::STAGE, NQ = C::NQM, QW = C::QW;
-  static_assert(C::STAGES == 3, "three LDS stages");
-  __shared__ __attribute__((aligned(1024))) char smem[3 * STAGE];
+  constexpr int S = C::STAGES;  // 2 or 3
+  __shared__ __attribute__((aligned(1024))) char smem[S * STAGE];
   auto swz = [](int row) { return ((row >> 3) & 1) << 1; };
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -445,7 +445,7 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6q_kernel(X6Args p) {
     const int k0 = kt * 32;
     const int seg = k0 / p.din, col0 = k0 - seg * p.din;
     const int shift = (int)(signed char)(p.off_packed >> (8 * seg));
-    char *st = smem + (kt % 3) * STAGE;
+    char *st = smem + (kt % S) * STAGE;
     const char *wbase = reinterpret_cast<const char *>(p.w) + (size_t)k0 * 2;
     const char *xbase = reinterpret_cast<const char *>(p.x) + (size_t)col0 * 2;
 #pragma unroll
@@ -477,19 +477,19 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6q_kernel(X6Args p) {
   };
 
   bf16x8 a0[2][TW], b0[2][TF], a1[TW], b1[TF], a2[TW], b2[TF];
-  issue(0);
-  issue(1);
-  issue(2);
-  wait_vmcnt<2 * NQ>();
+#pragma unroll
+  for (int t = 0; t < S; ++t) issue(t);
+  wait_vmcnt<(S - 1) * NQ>();
   __builtin_amdgcn_s_barrier();
   rd(smem, 0, a0[0], b0[0]);
 
-  // Step kt reads stage kt % 3: planes 1 and 2 before its barrier (plane 0
+  // Step kt reads stage kt % S: planes 1 and 2 before its barrier (plane 0
   // was read at the end of step kt-1), so once every wave has drained its
   // LDS reads (lgkmcnt(0)) and passed the barrier the stage is free and tile
-  // kt+3 is issued into it -- two steps ahead of its first read.  RAW: tile
-  // kt+1 is read (plane 0) right after the barrier; every wave's vmcnt(NQ)
-  // before it retired all but the newest issue (tile kt+2), i.e. tile kt+1.
+  // kt+S is issued into it -- S-1 steps ahead of its first read.  RAW: tile
+  // kt+1 is read (plane 0) right after the barrier; every wave's
+  // vmcnt((S-2) NQ) before it retired all but the newest S-2 issues (tiles
+  // kt+2 .. kt+S-1), i.e. tile kt+1.
   // In the last steps the issued tile is clamped to ktiles-1: a refetch of
   // the last tile into the stage it already occupies, writing the bytes it
   // holds, so any read of that stage sees the same values; it keeps one
@@ -497,7 +497,7 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6q_kernel(X6Args p) {
   // the nonexistent tile ktiles is never used.
   auto body = [&](int kt, auto cc) {
     constexpr int c = decltype(cc)::value;
-    const char *st = smem + (kt % 3) * STAGE;
+    const char *st = smem + (kt % S) * STAGE;
     rd(st, 1, a1, b1);
     mm(a0[c], b0[c]);
     rd(st, 2, a2, b2);
@@ -505,10 +505,10 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6q_kernel(X6Args p) {
     mm(a1, b0[c]);
     mm(a1, b1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    wait_vmcnt<NQ>();
+    wait_vmcnt<(S - 2) * NQ>();
     __builtin_amdgcn_s_barrier();
-    issue(kt + 3);
-    rd(smem + ((kt + 1) % 3) * STAGE, 0, a0[c ^ 1], b0[c ^ 1]);
+    issue(kt + S);
+    rd(smem + ((kt + 1) % S) * STAGE, 0, a0[c ^ 1], b0[c ^ 1]);
     mm(a0[c], b2);
     mm(a2, b0[c]);
     if constexpr (SCHED == 1) {
@@ -867,6 +867,18 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
       return launch_q<X6Cfg<128, 128, 4, 4, 3>, 0>(s, p, out16);
     case 25:
       return launch_q<X6Cfg<128, 128, 8, 2, 3>, 0>(s, p, out16);
+    case 26:
+      return launch_q<X6Cfg<256, 128, 4, 2, 2>, 0>(s, p, out16);
+    case 27:
+      return launch_q<X6Cfg<128, 256, 2, 4, 2>, 0>(s, p, out16);
+    case 28:
+      return launch_q<X6Cfg<128, 128, 4, 2, 2>, 0>(s, p, out16);
+    case 29:
+      return launch_q<X6Cfg<64, 128, 2, 2, 2>, 0>(s, p, out16);
+    case 30:
+      return launch_q<X6Cfg<128, 64, 2, 2, 2>, 0>(s, p, out16);
+    case 31:
+      return launch_q<X6Cfg<64, 128, 1, 4, 2>, 0>(s, p, out16);
     case 13:
       return launch_cfg<X6Cfg<128, 128, 2, 2, 2>>(s, p, out16);
     default:  // = 22
