@@ -538,6 +538,157 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6q_kernel(X6Args p) {
   x6_epilogue<TW, TF, OUT16>(p, acc, n0 + wrow, f0 + frow, lane);
 }
 
+// Staggered two-group schedule.  Each K-tile is three phases of 2 TW TF
+// MFMAs (w0x0 + w0x1 | w1x0 + w1x1 | w0x2 + w2x0); a phase is
+//   R: its fragment reads (+ up to half the wave's DMA pieces), barrier,
+//   M: lgkmcnt(0), the MFMAs at raised priority, barrier.
+// Waves 0-3 (group A) and 4-7 (group B, one of each per SIMD) run one
+// section apart: B passes one extra barrier before its first phase (A one
+// after its last), so while A multiplies B reads and issues DMAs and vice
+// versa -- the two waves of a SIMD alternate between the MFMA pipe and the
+// memory pipes instead of waiting on the same barrier for the same thing.
+//
+// Barrier instances (the joint prologue barrier = 0): A's phase q ends its R
+// section at instance 2q+1 and its M section at 2q+2; B's at 2q+2 and 2q+3.
+// A wave's reads of phase q are complete at the end of its M section
+// (lgkmcnt(0) there).  K-tile j = phases 3j .. 3j+2, all reading stage j % 3.
+//   WAR: stage (j-1) % 3 is last read in phase 3j-1, complete for A at
+//        instance 6j, for B at 6j+1.  Its refill (tile j+2) is issued in the
+//        R sections of phases 3j+1 and 3j+2, which start after instance
+//        6j+2 (A) / 6j+3 (B).
+//   RAW: tile j+1 is first read in phase 3j+3 (A: after instance 6j+6).
+//        Every wave retires its own pieces of tile j+1 at the end of the R
+//        section of phase 3j+2 (vmcnt: all but tile j+2's pieces), which is
+//        instance 6j+5 (A) / 6j+6 (B): before A's read, and B reads after
+//        6j+7.
+// Tiles past the end are clamped to the last one (a refetch of identical
+// bytes into the stage that holds it), so every step issues the same number
+// of pieces, which the vmcnt count relies on.
+template <class C, bool OUT16>
+__global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6z_kernel(X6Args p) {
+  constexpr int BW = C::BW, BF = C::BF, TW = C::TW, TF = C::TF;
+  constexpr int STAGE = C::STAGE, NQ = C::NQM, QW = C::QW;
+  static_assert(C::NW == 8 && C::STAGES == 3, "two groups of four waves, three stages");
+  static_assert(C::QW % C::NW == 0 && C::QF % C::NW == 0, "balanced pieces");
+  constexpr int NQ1 = (NQ + 1) / 2;  // pieces issued in phase 1, the rest in phase 2
+  __shared__ __attribute__((aligned(1024))) char smem[3 * STAGE];
+  auto swz = [](int row) { return ((row >> 3) & 1) << 1; };
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool groupB = wave >= 4;
+  const int ww = wave / C::WGF, wf = wave % C::WGF;
+  int tm, tn;
+  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
+  const int f0 = tm * BF, n0 = tn * BW;
+
+  const int lrow = lane >> 2, lch = lane & 3;
+  bool isw[NQ];
+  int piece[NQ];
+  uint32_t pconst[NQ];
+  int xrow[NQ];
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    isw[i] = i < C::NQW;
+    const int q = isw[i] ? wave * C::NQW + i : QW + wave * C::NQF + (i - C::NQW);
+    piece[i] = q;
+    if (isw[i]) {
+      const int plane = q / (BW / 16), row = (q % (BW / 16)) * 16 + lrow;
+      pconst[i] = (uint32_t)((min(n0 + row, p.n - 1) * p.ldw + plane * p.pw + 8 * (lch ^ swz(row))) * 2);
+      xrow[i] = 0;
+    } else {
+      const int q2 = q - QW, plane = q2 / (BF / 16), row = (q2 % (BF / 16)) * 16 + lrow;
+      pconst[i] = (uint32_t)((plane * p.px + 8 * (lch ^ swz(row))) * 2);
+      xrow[i] = f0 + row;
+    }
+  }
+  const int ktiles = p.kpad / 32;
+  // pieces lo .. hi-1 of tile kt (clamped)
+  auto issue = [&](int kt, auto lo_c, auto hi_c) {
+    constexpr int lo = decltype(lo_c)::value, hi = decltype(hi_c)::value;
+    kt = min(kt, ktiles - 1);
+    const int k0 = kt * 32;
+    const int seg = k0 / p.din, col0 = k0 - seg * p.din;
+    const int shift = (int)(signed char)(p.off_packed >> (8 * seg));
+    char *st = smem + (kt % 3) * STAGE;
+    const char *wbase = reinterpret_cast<const char *>(p.w) + (size_t)k0 * 2;
+    const char *xbase = reinterpret_cast<const char *>(p.x) + (size_t)col0 * 2;
+#pragma unroll
+    for (int i = lo; i < hi; ++i) {
+      const uint32_t xo = (uint32_t)(clampi(xrow[i] + shift, 0, p.m - 1) * p.ldx * 2) + pconst[i];
+      const char *src = isw[i] ? wbase + pconst[i] : xbase + xo;
+      glds16(src, st + piece[i] * 1024);
+    }
+  };
+
+  const int foff = (lane & 15) * 64 + (((lane >> 4) ^ (((lane >> 3) & 1) << 1)) * 16);
+  const int wrow = ww * TW * 16, frow = wf * TF * 16;
+  auto rda = [&](const char *st, int pl, bf16x8 *a) {
+#pragma unroll
+    for (int i = 0; i < TW; ++i) a[i] = *reinterpret_cast<const bf16x8 *>(st + (pl * BW + wrow + i * 16) * 64 + foff);
+  };
+  auto rdb = [&](const char *st, int pl, bf16x8 *b) {
+#pragma unroll
+    for (int j = 0; j < TF; ++j)
+      b[j] = *reinterpret_cast<const bf16x8 *>(st + 3 * BW * 64 + (pl * BF + frow + j * 16) * 64 + foff);
+  };
+  f32x4 acc[TW][TF];
+#pragma unroll
+  for (int i = 0; i < TW; ++i)
+#pragma unroll
+    for (int j = 0; j < TF; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  auto mm = [&](const bf16x8 *a, const bf16x8 *b) {
+#pragma unroll
+    for (int i = 0; i < TW; ++i)
+#pragma unroll
+      for (int j = 0; j < TF; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+  };
+  auto msect = [&](auto f) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    f();
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  bf16x8 a0[TW], a1[TW], a2[TW], b0[TF], b1[TF], b2[TF];
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, NQ1>;
+  using I2 = std::integral_constant<int, NQ>;
+  issue(0, I0(), I2());
+  issue(1, I0(), I2());
+  wait_vmcnt<NQ>();
+  __builtin_amdgcn_s_barrier();           // instance 0
+  if (groupB) __builtin_amdgcn_s_barrier();  // B: one section behind
+
+  for (int kt = 0; kt < ktiles; ++kt) {
+    const char *st = smem + (kt % 3) * STAGE;
+    // phase 0: w0x0 + w0x1
+    rda(st, 0, a0);
+    rdb(st, 0, b0);
+    rdb(st, 1, b1);
+    __builtin_amdgcn_s_barrier();
+    msect([&] { mm(a0, b0); mm(a0, b1); });
+    // phase 1: w1x0 + w1x1; first half of tile kt+2's pieces
+    rda(st, 1, a1);
+    issue(kt + 2, I0(), I1());
+    __builtin_amdgcn_s_barrier();
+    msect([&] { mm(a1, b0); mm(a1, b1); });
+    // phase 2: w0x2 + w2x0; the rest of tile kt+2, then retire tile kt+1
+    rda(st, 2, a2);
+    rdb(st, 2, b2);
+    issue(kt + 2, I1(), I2());
+    wait_vmcnt<NQ>();
+    __builtin_amdgcn_s_barrier();
+    msect([&] { mm(a0, b2); mm(a2, b0); });
+  }
+  if (!groupB) __builtin_amdgcn_s_barrier();  // A: match B's extra barrier
+  wait_vmcnt<0>();
+
+  x6_epilogue<TW, TF, OUT16>(p, acc, n0 + wrow, f0 + frow, lane);
+}
+
 // Register-staged schedule: operands travel global -> VGPR (plain
 // global_load_dwordx4) -> LDS (ds_write_b128) instead of LDS-DMA.  An LDS-DMA
 // piece costs its wave 60-185 issue cycles (MI355X_MICROARCH.md, constants
@@ -734,6 +885,19 @@ int launch_q(hipStream_t s, X6Args p, bool out16) {
 }
 
 template <class C>
+int launch_z(hipStream_t s, X6Args p, bool out16) {
+  p.tiles_n = (p.n + C::BW - 1) / C::BW;
+  p.tiles_m = (p.m + C::BF - 1) / C::BF;
+  dim3 grid(p.tiles_m * p.tiles_n), block(C::NT);
+  if (out16)
+    hipLaunchKernelGGL((gemm_bf16x6z_kernel<C, true>), grid, block, 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_bf16x6z_kernel<C, false>), grid, block, 0, s, p);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
+template <class C>
 int launch_reg(hipStream_t s, X6Args p, bool out16) {
   p.tiles_n = (p.n + C::BW - 1) / C::BW;
   p.tiles_m = (p.m + C::BF - 1) / C::BF;
@@ -879,6 +1043,10 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
       return launch_q<X6Cfg<128, 64, 2, 2, 2>, 0>(s, p, out16);
     case 31:
       return launch_q<X6Cfg<64, 128, 1, 4, 2>, 0>(s, p, out16);
+    case 32:
+      return launch_z<X6Cfg<128, 128, 4, 2, 3>>(s, p, out16);
+    case 33:
+      return launch_z<X6Cfg<128, 128, 2, 4, 3>>(s, p, out16);
     case 13:
       return launch_cfg<X6Cfg<128, 128, 2, 2, 2>>(s, p, out16);
     default:  // = 22
