@@ -138,14 +138,18 @@ def gemm_algorithmic_bytes(rows, layers=((3072, 1024),) * 4 + ((1024, 1024), (10
     return sum(4 * (rows * k + k * n + rows * n) for k, n in layers) / len(layers)
 
 
-def split_algorithmic_bytes(rows, eb, layers=((256, 1024),) + ((3072, 1024),) * 4 + ((1024, 1024), (1024, 3456))):
+def split_algorithmic_bytes(rows, eb, layers=((256, 1024),) + ((3072, 1024),) * 4 + ((1024, 1024), (1024, 3456)),
+                            hidden_only=False):
     """Split-plane GEMM operands per launch on average over TDNN-S layers
-    1-7: A and W at eb bytes per element (6: three bf16 planes, 4: two fp16
-    planes; A counted once per row and segment), hidden outputs written split,
-    the last as fp32."""
+    1-7 (or the six hidden layers 1-6, whose launches are the split-output
+    instantiation the PMC traffic is quoted for): A and W at eb bytes per
+    element (6: three bf16 planes, 4: two fp16 planes; A counted once per row
+    and segment), hidden outputs written split, the last as fp32."""
+    if hidden_only:
+        layers = layers[:-1]
     tot = 0
     for i, (k, n) in enumerate(layers):
-        out = 4 if i == len(layers) - 1 else eb
+        out = 4 if i == 6 else eb
         tot += eb * rows * k + eb * k * n + out * rows * n
     return tot / len(layers)
 
@@ -485,12 +489,16 @@ def main():
                         "mfma_16bit_tflops": round(achieved * prods, 1),
                         "vs_fp32_mfma_peak": round(achieved / MFMA_F32_PEAK_TFLOPS, 4),
                         "traffic": traffic, "traffic_source": src,
-                        "kernel": SPLIT_ROOFLINE_KERNEL[split] + " (TDNN-S layers 1-7)",
+                        "kernel": SPLIT_ROOFLINE_KERNEL[split] + " + its fp32-output form (TDNN-S layers 1-7; "
+                                  "rocprof: tools/trace_summary.py 'kernel template' union)",
                         "launches": n, "avg_launch_ms": round(ms / n, 4), "busy_ms": round(busy, 3),
                         "effective_ms_per_launch": round(busy / n, 4),
                         "flops_per_launch": flops_per_launch,
                         "algorithmic_bytes_per_launch": split_algorithmic_bytes(
-                            plan.max_chunk_rows, {"bf16x6": 6, "f16x3": 4}[split])}
+                            plan.max_chunk_rows, {"bf16x6": 6, "f16x3": 4}[split]),
+                        "traffic_scope": "PMC bytes per hidden-layer launch (split-output instantiation, "
+                                         "layers 1-6); algorithmic bytes of the same launches: "
+                                         f"{split_algorithmic_bytes(plan.max_chunk_rows, {'bf16x6': 6, 'f16x3': 4}[split], hidden_only=True):.4g}"}
         elif n:
             # With several nnet streams, launches of this kernel overlap each
             # other; a launch's own duration then includes time shared with

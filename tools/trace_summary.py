@@ -47,6 +47,16 @@ def main(path, title=""):
     for k, iv in sorted(by_name.items(), key=lambda kv: -sum(b - a for a, b in kv[1])):
         n = len(iv)
         print(f"{k[:88]:88s} {n:5d} {sum(b - a for a, b in iv)/n:8.1f} {union_us(iv)/n:16.1f}")
+    # one kernel template, every instantiation (e.g. a GEMM's hidden-layer
+    # and last-layer forms): bench.py's roofline unions over all of them
+    by_tmpl = defaultdict(list)
+    for name, iv in by_name.items():
+        by_tmpl[name.split("<")[0]] += iv
+    print()
+    print(f"{'kernel template (all instantiations)':88s} {'n':>5s} {'mean_us':>8s} {'union_us/launch':>16s}")
+    for k, iv in sorted(by_tmpl.items(), key=lambda kv: -sum(b - a for a, b in kv[1])):
+        n = len(iv)
+        print(f"{k[:88]:88s} {n:5d} {sum(b - a for a, b in iv)/n:8.1f} {union_us(iv)/n:16.1f}")
 
 
 if __name__ == "__main__":
