@@ -119,12 +119,13 @@ def cpu_baseline(conf, n_utts, seconds, threads, min_wall):
 ROOFLINE_KERNEL = "gemm_f32_glds_kernel<catears::Cfg<128, 64, 32, 2, 2>, 2, false>"
 # split-plane hidden layers (split output), the default variants
 SPLIT_ROOFLINE_KERNEL = {
-    "bf16x6": "gemm_bf16x6q_kernel<catears::X6Cfg<128, 128, 4, 2, 3>, true, 0>",
+    "bf16x6": "gemm_bf16x6f_kernel<catears::X6Cfg<128, 256, 2, 4, 2> >",
     "f16x3": "gemm_f16x3_kernel<catears::X3Cfg<128, 128, 2, 4, 2, 64>, true>",
 }
 SPLIT_DTYPE = {
     "bf16x6": "fp32 (bf16x6 GEMM: fp32 operands split exactly into 3 bf16 planes, 6 MFMA products, fp32 "
-              "accumulate; error vs oracle at the fp32-MFMA path's level, tests/test_gpu_parity.py)",
+              "accumulate; every operand bit kept, dropped cross terms < 2^-25 |w x|; error vs oracle at the "
+              "fp32-MFMA path's level, tests/test_gpu_parity.py)",
     "f16x3": "fp32 (f16x3 GEMM: fp32 operands scaled by powers of two and split into 2 fp16 planes, 22-23 "
              "significant bits, 3 MFMA products in 2 fp32 accumulators; error vs oracle at the fp32-MFMA "
              "path's level, tests/test_gpu_parity.py)",
@@ -143,8 +144,9 @@ def split_algorithmic_bytes(rows, eb, layers=((256, 1024),) + ((3072, 1024),) * 
     """Split-plane GEMM operands per launch on average over TDNN-S layers
     1-7 (or the six hidden layers 1-6, whose launches are the split-output
     instantiation the PMC traffic is quoted for): A and W at eb bytes per
-    element (6: three bf16 planes, 4: two fp16 planes; A counted once per row
-    and segment), hidden outputs written split, the last as fp32."""
+    element (6: three bf16 planes, 4: two fp16 planes or fp32 operands; A
+    counted once per row and segment), hidden outputs written at eb bytes, the
+    last as fp32."""
     if hidden_only:
         layers = layers[:-1]
     tot = 0
@@ -480,7 +482,14 @@ def main():
             peak = MFMA_BF16_PEAK_TFLOPS / prods
             flops_per_launch = frames_per_step * FLOPS_PER_FRAME / (n / args.steps)
             achieved = flops_per_launch * n / (busy * 1e-3) / 1e12
-            traffic, src = pmc_traffic(SPLIT_ROOFLINE_KERNEL[split])
+            # bf16x6 default: fp32 operands split on the way into LDS, one
+            # kernel instantiation for every layer (CATEARS_X6_F32IN=0: the
+            # plane-operand kernels, hidden layers in their split-output form)
+            f32in = split == "bf16x6" and os.environ.get("CATEARS_X6_F32IN", "1") != "0"
+            kname = SPLIT_ROOFLINE_KERNEL[split] if f32in or split != "bf16x6" else \
+                "gemm_bf16x6q_kernel<catears::X6Cfg<128, 128, 4, 2, 3>, true, 0>"
+            traffic, src = pmc_traffic(kname)
+            eb = 4 if f32in else {"bf16x6": 6, "f16x3": 4}[split]
             roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1),
                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                         "peak_basis": f"{'bf16' if split == 'bf16x6' else 'fp16'} dense MFMA "
@@ -489,16 +498,17 @@ def main():
                         "mfma_16bit_tflops": round(achieved * prods, 1),
                         "vs_fp32_mfma_peak": round(achieved / MFMA_F32_PEAK_TFLOPS, 4),
                         "traffic": traffic, "traffic_source": src,
-                        "kernel": SPLIT_ROOFLINE_KERNEL[split] + " + its fp32-output form (TDNN-S layers 1-7; "
-                                  "rocprof: tools/trace_summary.py 'kernel template' union)",
+                        "kernel": kname + (" (every TDNN-S Linear, layers 1-7; rocprof: tools/trace_summary.py)"
+                                           if f32in else " + its fp32-output form (TDNN-S layers 1-7; rocprof: "
+                                           "tools/trace_summary.py 'kernel template' union)"),
                         "launches": n, "avg_launch_ms": round(ms / n, 4), "busy_ms": round(busy, 3),
                         "effective_ms_per_launch": round(busy / n, 4),
                         "flops_per_launch": flops_per_launch,
-                        "algorithmic_bytes_per_launch": split_algorithmic_bytes(
-                            plan.max_chunk_rows, {"bf16x6": 6, "f16x3": 4}[split]),
-                        "traffic_scope": "PMC bytes per hidden-layer launch (split-output instantiation, "
-                                         "layers 1-6); algorithmic bytes of the same launches: "
-                                         f"{split_algorithmic_bytes(plan.max_chunk_rows, {'bf16x6': 6, 'f16x3': 4}[split], hidden_only=True):.4g}"}
+                        "algorithmic_bytes_per_launch": split_algorithmic_bytes(plan.max_chunk_rows, eb),
+                        "traffic_scope": ("PMC bytes per launch averaged over all 7 layers (fp32 operands)" if f32in else
+                                          "PMC bytes per hidden-layer launch (split-output instantiation, layers "
+                                          "1-6); algorithmic bytes of the same launches: "
+                                          f"{split_algorithmic_bytes(plan.max_chunk_rows, eb, hidden_only=True):.4g}")}
         elif n:
             # With several nnet streams, launches of this kernel overlap each
             # other; a launch's own duration then includes time shared with

@@ -1027,6 +1027,77 @@ static int run_steps_f32(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
 // The bf16x6 program (kernels/gemm_bf16x6.hip): the first layer's spliced
 // block is written as three bf16 planes, every hidden layer's epilogue
 // writes its output split for the next, the last layer writes fp32.
+// bf16x6 with fp32 operands in HBM (gemm_bf16x6f_kernel: the split into
+// planes happens on the way into LDS): the layers chain fp32 activations as
+// the fp32 program does, the weights are the fp32 `wt` matrices.  4 B per
+// operand element through L2 instead of the planes' 6; measured +3 % over
+// the plane kernels (tools/ab.sh).
+// Default; CATEARS_X6_F32IN=0 selects the plane-operand kernels
+// (run_steps_x6: planes written by each epilogue, bit-identical results).
+static bool x6_f32in() {
+  static const bool v = [] {
+    const char *e = getenv("CATEARS_X6_F32IN");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
+
+static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, int ldx, int rows,
+                         const int *row_map, const float **y, int *ldy) {
+  int max_in = 0;
+  for (const Step &st : m->steps) max_in = std::max(max_in, st.gemm.kpad);
+  for (const Step &st : m->steps) max_in = std::max(max_in, (st.gemm.n + 31) / 32 * 32);
+  const size_t blk = ((size_t)rows * max_in + 63) / 64 * 64;
+  CE_TRY(ensure_workspace(ctx, 2 * blk + (size_t)rows * m->num_pdfs));
+  float *buf[2] = {ctx->workspace.as<float>(), ctx->workspace.as<float>() + blk};
+  float *out = ctx->workspace.as<float>() + 2 * blk;
+  const float *xs = nullptr;
+  int px = 0, cur = 0;
+  for (size_t i = 0; i < m->steps.size(); ++i) {
+    const GemmLayer &g = m->steps[i].gemm;
+    const bool last = i + 1 == m->steps.size();
+    X6Gemm a;
+    if (i == 0) {
+      ProfScope prof(ctx, CE_GPU_PROF_GEMM_GATHER);
+      CE_TRY(launch_splice_pad(ctx->stream, x, ldx, rows, g.din, g.nseg, g.off, row_map, buf[cur], g.kpad));
+      xs = buf[cur];
+      px = g.kpad;
+      cur ^= 1;
+      a.din = g.kpad;
+      a.nseg = 1;
+    } else {
+      a.din = g.din;
+      a.nseg = g.nseg;
+      for (int s = 0; s < 8; ++s) a.off[s] = g.off[s];
+    }
+    a.xf = xs;
+    a.ldx = px;
+    a.wf = g.wt.as<float>();
+    a.ldw = g.kpad;
+    a.m = rows;
+    a.n = g.n;
+    a.kpad = i == 0 ? g.kpad : g.nseg * g.din;
+    a.bias = g.bias.as<float>();
+    a.bn_scale = g.bn_scale.as<float>();
+    a.bn_offset = g.bn_offset.as<float>();
+    for (int q = 0; q < 4; ++q) a.post[q] = g.post[q];
+    a.npost = g.npost;
+    const int pn = (g.n + 31) / 32 * 32;
+    a.y32 = last ? out : buf[cur];
+    a.ldy = last ? g.n : pn;
+    {
+      ProfScope prof(ctx, CE_GPU_PROF_GEMM);
+      CE_TRY(launch_gemm_bf16x6(ctx->stream, a));
+    }
+    xs = buf[cur];
+    px = pn;
+    cur ^= 1;
+  }
+  *y = out;
+  *ldy = m->steps.back().gemm.n;
+  return CE_GPU_OK;
+}
+
 static int run_steps_x6(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, int ldx, int rows,
                         const int *row_map, const float **y, int *ldy) {
   int max_in = 0;
@@ -1232,7 +1303,9 @@ static int run_steps(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, int
                      const int *row_map, const uint32_t *row_edge, const float **y, int *ldy) {
   if (m->int8) return run_steps_i8(ctx, m, x, ldx, rows, row_map, row_edge, y, ldy);
   if (m->gemm == CE_GPU_GEMM_F16X3) return run_steps_x3(ctx, m, x, ldx, rows, row_map, y, ldy);
-  if (m->gemm == CE_GPU_GEMM_BF16X6) return run_steps_x6(ctx, m, x, ldx, rows, row_map, y, ldy);
+  if (m->gemm == CE_GPU_GEMM_BF16X6)
+    return x6_f32in() ? run_steps_x6f(ctx, m, x, ldx, rows, row_map, y, ldy)
+                      : run_steps_x6(ctx, m, x, ldx, rows, row_map, y, ldy);
   return run_steps_f32(ctx, m, x, ldx, rows, row_map, y, ldy);
 }
 

@@ -315,6 +315,10 @@ struct X6Gemm {
   int ldx = 0, px = 0;
   const uint16_t *w = nullptr;
   int ldw = 0, pw = 0;
+  // fp32 operands instead (xf rows x ldx floats, wf n x ldw floats, both
+  // K-contiguous): split into the three planes on the way into LDS; the
+  // output is then fp32 (y32) for every layer
+  const float *xf = nullptr, *wf = nullptr;
   int m = 0, n = 0, kpad = 0, din = 0, nseg = 1;
   int off[8] = {0};
   const float *bias = nullptr, *bn_scale = nullptr, *bn_offset = nullptr;

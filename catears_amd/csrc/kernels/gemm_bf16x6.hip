@@ -57,6 +57,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 struct X6Args {
   const uint16_t *w;  // weights, n x ldw, plane stride pw (elements)
   const uint16_t *x;  // activations, rows x ldx, plane stride px
+  const float *wf, *xf;  // or fp32 operands (gemm_bf16x6f_kernel; ldw / ldx in floats)
   const float *bias, *bn_scale, *bn_offset;
   float *y32;         // fp32 output (ldy floats per row), or
   uint16_t *y16;      // split output (ldy elements per row, plane stride py)
@@ -689,6 +690,151 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6z_kernel(X6Args p) {
   x6_epilogue<TW, TF, OUT16>(p, acc, n0 + wrow, f0 + frow, lane);
 }
 
+// fp32-in schedule: operands stay fp32 in HBM (4 B per element instead of
+// the planes' 6) and are split into the three bf16 planes on their way into
+// LDS.  The split/plane kernels above are bound by the bytes the L2 can move
+// into LDS (f16x3's 4 B per element runs at 6/4 of their fp32-FLOP rate with
+// half the MFMA work), so the fill carries fp32 and the VALU pays for the
+// split, interleaved with the MFMAs.  Per K-tile each thread loads 8
+// consecutive floats of one weight row and of one activation row (one 128-B
+// line per row across 4 threads; global_load_dwordx4 x 2), splits them with
+// the same split3 as the epilogue (so the planes -- and the results -- are
+// bit-identical to the plane path), and writes 16 B per plane with
+// ds_write_b128 into the layout the fragment reads expect.  Two LDS stages,
+// registers one tile ahead:
+//   step kt: write tile kt+1 (loaded during step kt-1) into stage (kt+1) % 2,
+//            load tile kt+2 into registers, fragment reads + MFMAs of stage
+//            kt % 2, lgkmcnt(0), raw s_barrier (no vmcnt: the loads stay in
+//            flight across it).
+//   WAR: stage (kt+1) % 2 was read in step kt-1, whose reads all fed MFMAs
+//        before that step's barrier.  RAW: the writes of tile kt+1 are
+//        drained before step kt's barrier; step kt+1 reads after it.
+// Tiles past the end are clamped to the last one (written to a stage no
+// later step reads), so the body is one basic block.
+template <class C>
+__global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
+  constexpr int BW = C::BW, BF = C::BF, TW = C::TW, TF = C::TF, NT = C::NT, STAGE = C::STAGE;
+  constexpr int RPP = NT / 4;  // rows per pass (4 threads x 32 B per row)
+  static_assert(BW % RPP == 0 && BF % RPP == 0, "rows per pass");
+  constexpr int NPW = BW / RPP, NPX = BF / RPP;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  auto swz = [](int row) { return ((row >> 3) & 1) << 1; };
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ww = wave / C::WGF, wf = wave % C::WGF;
+  int tm, tn;
+  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
+  const int f0 = tm * BF, n0 = tn * BW;
+  const int prow = tid >> 2, pch = tid & 3;
+
+  typedef const __attribute__((address_space(1))) f32x4v gvec;
+  uint32_t wsrc[NPW];  // float offset of this thread's weight row at k = 0
+#pragma unroll
+  for (int i = 0; i < NPW; ++i) wsrc[i] = (uint32_t)(min(n0 + prow + i * RPP, p.n - 1) * p.ldw + 8 * pch);
+  const int ktiles = p.kpad / 32;
+  f32x4v rw0[NPW], rw1[NPW], rx0[NPX], rx1[NPX];
+  auto load = [&](int kt) {
+    kt = min(kt, ktiles - 1);
+    const int k0 = kt * 32;
+    const int seg = k0 / p.din, col0 = k0 - seg * p.din;
+    const int shift = (int)(signed char)(p.off_packed >> (8 * seg));
+    gvec *wb = (gvec *)(p.wf + k0);
+#pragma unroll
+    for (int i = 0; i < NPW; ++i) {
+      rw0[i] = wb[wsrc[i] / 4];
+      rw1[i] = wb[wsrc[i] / 4 + 1];
+    }
+    gvec *xb = (gvec *)(p.xf + col0 + 8 * pch);
+#pragma unroll
+    for (int i = 0; i < NPX; ++i) {
+      const int src = clampi(f0 + prow + i * RPP + shift, 0, p.m - 1);
+      const uint32_t o = (uint32_t)(src * p.ldx) / 4;
+      rx0[i] = xb[o];
+      rx1[i] = xb[o + 1];
+    }
+  };
+  // 8 floats -> three 16-B plane chunks at row r of the plane block `base`
+  auto put = [&](char *base, int nrows, int r, f32x4v v0, f32x4v v1) {
+    u32x4 h, m, l;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      uint16_t h0, m0, l0, h1, m1, l1;
+      const f32x4v &v = e < 2 ? v0 : v1;
+      split3(v[(2 * e) & 3], &h0, &m0, &l0);
+      split3(v[(2 * e + 1) & 3], &h1, &m1, &l1);
+      h[e] = h0 | ((uint32_t)h1 << 16);
+      m[e] = m0 | ((uint32_t)m1 << 16);
+      l[e] = l0 | ((uint32_t)l1 << 16);
+    }
+    const int off = r * 64 + ((pch ^ swz(r)) * 16);
+    *reinterpret_cast<u32x4 *>(base + off) = h;
+    *reinterpret_cast<u32x4 *>(base + nrows * 64 + off) = m;
+    *reinterpret_cast<u32x4 *>(base + 2 * nrows * 64 + off) = l;
+  };
+  auto store = [&](int kt) {
+    char *st = smem + (kt & 1) * STAGE;
+#pragma unroll
+    for (int i = 0; i < NPW; ++i) put(st, BW, prow + i * RPP, rw0[i], rw1[i]);
+#pragma unroll
+    for (int i = 0; i < NPX; ++i) put(st + 3 * BW * 64, BF, prow + i * RPP, rx0[i], rx1[i]);
+  };
+
+  const int foff = (lane & 15) * 64 + (((lane >> 4) ^ (((lane >> 3) & 1) << 1)) * 16);
+  const int wrow = ww * TW * 16, frow = wf * TF * 16;
+  f32x4 acc[TW][TF];
+#pragma unroll
+  for (int i = 0; i < TW; ++i)
+#pragma unroll
+    for (int j = 0; j < TF; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+
+  load(0);
+  store(0);
+  load(1);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < ktiles; ++kt) {
+    store(kt + 1);
+    load(kt + 2);
+    const char *st = smem + (kt & 1) * STAGE;
+    bf16x8 a[3][TW], b[3][TF];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+      for (int i = 0; i < TW; ++i)
+        a[pl][i] = *reinterpret_cast<const bf16x8 *>(st + (pl * BW + wrow + i * 16) * 64 + foff);
+#pragma unroll
+      for (int j = 0; j < TF; ++j)
+        b[pl][j] = *reinterpret_cast<const bf16x8 *>(st + 3 * BW * 64 + (pl * BF + frow + j * 16) * 64 + foff);
+    }
+#pragma unroll
+    for (int i = 0; i < TW; ++i)
+#pragma unroll
+      for (int j = 0; j < TF; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < TW; ++i)
+#pragma unroll
+      for (int j = 0; j < TF; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[1][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[0][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[1][j], acc[i][j], 0, 0, 0);
+      }
+#pragma unroll
+    for (int i = 0; i < TW; ++i)
+#pragma unroll
+      for (int j = 0; j < TF; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[2][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2][i], b[0][j], acc[i][j], 0, 0, 0);
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  x6_epilogue<TW, TF, false>(p, acc, n0 + wrow, f0 + frow, lane);
+}
+
 // Register-staged schedule: operands travel global -> VGPR (plain
 // global_load_dwordx4) -> LDS (ds_write_b128) instead of LDS-DMA.  An LDS-DMA
 // piece costs its wave 60-185 issue cycles (MI355X_MICROARCH.md, constants
@@ -898,6 +1044,16 @@ int launch_z(hipStream_t s, X6Args p, bool out16) {
 }
 
 template <class C>
+int launch_f(hipStream_t s, X6Args p) {
+  p.tiles_n = (p.n + C::BW - 1) / C::BW;
+  p.tiles_m = (p.m + C::BF - 1) / C::BF;
+  dim3 grid(p.tiles_m * p.tiles_n), block(C::NT);
+  hipLaunchKernelGGL((gemm_bf16x6f_kernel<C>), grid, block, 0, s, p);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
+template <class C>
 int launch_reg(hipStream_t s, X6Args p, bool out16) {
   p.tiles_n = (p.n + C::BW - 1) / C::BW;
   p.tiles_m = (p.m + C::BF - 1) / C::BF;
@@ -926,15 +1082,24 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
     return fail(CE_GPU_EINVAL, "gemm_bf16x6: bad K geometry");
   if (a.n % 4 != 0 || a.ldy % 4 != 0 || (a.y16 && a.py % 4 != 0))
     return fail(CE_GPU_EINVAL, "gemm_bf16x6: output width must be a multiple of 4");
-  if (a.ldw % 8 || a.pw % 8 || a.ldx % 8 || a.px % 8 || (reinterpret_cast<uintptr_t>(a.w) & 15) ||
-      (reinterpret_cast<uintptr_t>(a.x) & 15))
-    return fail(CE_GPU_EINVAL, "gemm_bf16x6: operands must be 16-byte aligned");
-  if ((int64_t)a.n * a.ldw * 2 >= ((int64_t)1 << 32) || (int64_t)a.m * a.ldx * 2 >= ((int64_t)1 << 32))
-    return fail(CE_GPU_EINVAL, "gemm_bf16x6: operand beyond 4 GiB");
+  const bool f32in = a.xf != nullptr;
+  if (f32in) {
+    if (!a.wf || !a.y32 || a.ldw % 4 || a.ldx % 4 || (reinterpret_cast<uintptr_t>(a.wf) & 15) ||
+        (reinterpret_cast<uintptr_t>(a.xf) & 15))
+      return fail(CE_GPU_EINVAL, "gemm_bf16x6: fp32 operands must be 16-byte aligned, output fp32");
+  } else {
+    if (a.ldw % 8 || a.pw % 8 || a.ldx % 8 || a.px % 8 || (reinterpret_cast<uintptr_t>(a.w) & 15) ||
+        (reinterpret_cast<uintptr_t>(a.x) & 15))
+      return fail(CE_GPU_EINVAL, "gemm_bf16x6: operands must be 16-byte aligned");
+    if ((int64_t)a.n * a.ldw * 2 >= ((int64_t)1 << 32) || (int64_t)a.m * a.ldx * 2 >= ((int64_t)1 << 32))
+      return fail(CE_GPU_EINVAL, "gemm_bf16x6: operand beyond 4 GiB");
+  }
   if (a.npost > 4) return fail(CE_GPU_EINVAL, "gemm_bf16x6: too many post ops");
   X6Args p;
   p.w = a.w;
   p.x = a.x;
+  p.wf = a.wf;
+  p.xf = a.xf;
   p.bias = a.bias;
   p.bn_scale = a.bn_scale;
   p.bn_offset = a.bn_offset;
@@ -960,6 +1125,18 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
   p.post_mode = post_mode(a.post, a.npost);
   p.group = 8;
   const bool out16 = a.y16 != nullptr;
+  if (f32in) {
+    switch (x6_variant()) {
+      case 40:
+        return launch_f<X6Cfg<128, 128, 4, 2, 2>>(s, p);
+      case 41:
+        return launch_f<X6Cfg<128, 128, 2, 4, 2>>(s, p);
+      case 43:
+        return launch_f<X6Cfg<256, 128, 4, 2, 2>>(s, p);
+      default:  // = 42
+        return launch_f<X6Cfg<128, 256, 2, 4, 2>>(s, p);
+    }
+  }
   switch (x6_variant()) {
     case 1:
       return launch_cfg<X6Cfg<128, 128, 2, 2, 3>>(s, p, out16);
