@@ -440,6 +440,112 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_i8_glds_kernel(I8Args 
 }
 
 
+// Branch-free form of gemm_i8_glds_kernel with three stages and the DMA two
+// K-tiles ahead (the structure of gemm_bf16x6q_kernel): step kt reads stage
+// kt % 3 (four k-steps), drains its LDS reads (lgkmcnt(0)), retires its own
+// pieces of tile kt+1 (vmcnt: all but tile kt+2's), passes one raw barrier
+// and issues tile kt+3 into the stage it just freed.  Tail tiles are clamped
+// to the last one (a refetch of identical bytes into the stage that holds
+// it), so every step issues the same pieces and the body is one basic block.
+template <int BM, int BN, int WGM, int WGN>
+__global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_i8_q_kernel(I8Args p) {
+  constexpr int NW = WGM * WGN;
+  constexpr int BKB = 128;
+  constexpr int TI = BM / WGM / 32, TJ = BN / WGN / 32;
+  constexpr int RPI = 1024 / BKB;
+  constexpr int NGA = BM * BKB / 1024 / NW, NGB = BN * BKB / 1024 / NW, NG = NGA + NGB;
+  constexpr int STAGE = (BM + BN) * BKB;
+  static_assert(NGA >= 1 && NGB >= 1 && TI >= 1 && TJ >= 1, "tile too small");
+  static_assert(3 * STAGE <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(1024))) int8_t smem[3 * STAGE];
+  auto swz = [](int row) { return (row >> 1) & 7; };
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN, r = lane & 31, h = lane >> 5;
+  int tm, tn;
+  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int lrow = lane / 8, lchunk = lane & 7;
+  uint32_t boff[NGB];
+#pragma unroll
+  for (int j = 0; j < NGB; ++j) {
+    const int row = (wave * NGB + j) * RPI + lrow;
+    boff[j] = (uint32_t)(min(n0 + row, p.n - 1) * p.kpad + 16 * (lchunk ^ swz(row)));
+  }
+  int arow[NGA];
+  uint32_t achunk[NGA];
+#pragma unroll
+  for (int i = 0; i < NGA; ++i) {
+    const int row = (wave * NGA + i) * RPI + lrow;
+    arow[i] = m0 + row;
+    achunk[i] = (uint32_t)(16 * (lchunk ^ swz(row)));
+  }
+  const int ktiles = p.kpad / BKB;
+  auto issue = [&](int kt) {
+    kt = min(kt, ktiles - 1);
+    const int k0 = kt * BKB;
+    const int seg = k0 / p.din, col0 = k0 - seg * p.din;
+    const int shift = p.off[seg < 8 ? seg : 7];
+    int8_t *st = smem + (kt % 3) * STAGE;
+    const char *abase = reinterpret_cast<const char *>(p.a) + col0;
+    const char *bbase = reinterpret_cast<const char *>(p.w) + k0;
+#pragma unroll
+    for (int i = 0; i < NGA; ++i) {
+      int src = arow[i] + shift;
+      src = src < 0 ? 0 : (src > p.m - 1 ? p.m - 1 : src);
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void *)(abase + (uint32_t)(src * p.lda) + achunk[i]),
+          (__attribute__((address_space(3))) void *)(st + (wave * NGA + i) * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < NGB; ++j)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(bbase + boff[j]),
+                                       (__attribute__((address_space(3))) void *)(st + BM * BKB + (wave * NGB + j) * 1024),
+                                       16, 0, 0);
+  };
+
+  i32x16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0;
+
+  const int xr = swz(r) ^ h;
+  const int a_row = (wm * TI * 32 + r) * BKB, b_row = BM * BKB + (wn * TJ * 32 + r) * BKB;
+  issue(0);
+  issue(1);
+  issue(2);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NG) : "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < ktiles; ++kt) {
+    const int8_t *st = smem + (kt % 3) * STAGE;
+#pragma unroll
+    for (int s = 0; s < BKB / 32; ++s) {
+      const int ch = ((2 * s) ^ xr) * 16;
+      i32x4 af[TI], bf[TJ];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) af[i] = *reinterpret_cast<const i32x4 *>(st + a_row + i * 32 * BKB + ch);
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) bf[j] = *reinterpret_cast<const i32x4 *>(st + b_row + j * 32 * BKB + ch);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NG) : "memory");
+    __builtin_amdgcn_s_barrier();
+    issue(kt + 3);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  i8_epilogue<TI, TJ, BM, 64 * NW>(p, acc, m0, wm * TI * 32, n0 + wn * TJ * 32, r, h, reinterpret_cast<uint32_t *>(smem));
+}
+
 // Register-staged form: the next K-tile is fetched with global_load_dwordx4
 // into VGPRs while the current one is multiplied, then written to the other
 // LDS buffer with ds_write_b128.  An LDS-DMA piece costs its wave ~60-180
@@ -635,6 +741,10 @@ int launch_i8_gemm(hipStream_t s, const I8Layer &L, const int8_t *a, int lda, in
       // (the loop waits on L2 / MALL fetches, 43 % of wave cycles parked, MFMA
       // busy ~20 %); 9 (128 tiles) leaves half the CUs idle when alone.
       case 15: go(gemm_i8_glds_kernel<256, 128, 3, 4, 2>, 256, 128, 512); break;
+      // 20-22: branch-free, DMA two K-tiles ahead (gemm_i8_q_kernel)
+      case 20: go(gemm_i8_q_kernel<256, 128, 4, 2>, 256, 128, 512); break;
+      case 21: go(gemm_i8_q_kernel<128, 256, 2, 4>, 128, 256, 512); break;
+      case 22: go(gemm_i8_q_kernel<128, 128, 2, 2>, 128, 128, 256); break;
       default: go(gemm_i8_glds_kernel<128, 128, 2>, 128, 128); break;
     }
     CE_HIP(hipGetLastError());
