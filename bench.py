@@ -37,7 +37,7 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: ~2.5 PF dense bf16 / fp1
 # Split-plane GEMMs (ce_gpu_model_set_gemm): bf16x6 issues six bf16 MFMA
 # products per fp32 multiply-add, f16x3 three fp16 ones, so the kernel's
 # ceiling in fp32 (algorithmic) FLOP/s is the 16-bit dense peak / products.
-SPLIT_PRODUCTS = {"bf16x6": 6, "f16x3": 3}
+SPLIT_PRODUCTS = {"bf16x6": 6, "bf16x6p": 6, "f16x3": 3}
 HBM_PEAK_GBS = 8000.0
 METRIC = "acoustic frames/sec (fbank->nnet posteriors), 16kHz, 1/2/4/8 GPU"
 
@@ -65,7 +65,7 @@ def parse():
                     help="c3: full pipeline fp32 (the headline metric); c2: batched fbank only, "
                          "1000 x 10 s utterances per step; c5: full pipeline with the int8 nnet path, "
                          "frame batch 8192")
-    ap.add_argument("--gemm", choices=["fp32", "bf16x6", "f16x3"], default=None,
+    ap.add_argument("--gemm", choices=["fp32", "bf16x6", "bf16x6p", "f16x3"], default=None,
                     help="matrix-core form of the fp32 Linear layers (ce_gpu_model_set_gemm); default: "
                          "the library's (bf16x6: three exact bf16 planes, six products, fp32 GEMM)")
     ap.add_argument("--back-streams", type=int, default=3,
@@ -120,12 +120,15 @@ ROOFLINE_KERNEL = "gemm_f32_glds_kernel<catears::Cfg<128, 64, 32, 2, 2>, 2, fals
 # split-plane hidden layers (split output), the default variants
 SPLIT_ROOFLINE_KERNEL = {
     "bf16x6": "gemm_bf16x6f_kernel<catears::X6Cfg<128, 256, 2, 4, 2> >",
+    "bf16x6p": "gemm_bf16x6q_kernel<catears::X6Cfg<128, 128, 4, 2, 3>, true, 0>",
     "f16x3": "gemm_f16x3_kernel<catears::X3Cfg<128, 128, 2, 4, 2, 64>, true>",
 }
 SPLIT_DTYPE = {
     "bf16x6": "fp32 (bf16x6 GEMM: fp32 operands split exactly into 3 bf16 planes, 6 MFMA products, fp32 "
               "accumulate; every operand bit kept, dropped cross terms < 2^-25 |w x|; error vs oracle at the "
               "fp32-MFMA path's level, tests/test_gpu_parity.py)",
+    "bf16x6p": "fp32 (bf16x6 GEMM with the planes stored in HBM: same products and order as bf16x6, "
+               "bit-identical results)",
     "f16x3": "fp32 (f16x3 GEMM: fp32 operands scaled by powers of two and split into 2 fp16 planes, 22-23 "
              "significant bits, 3 MFMA products in 2 fp32 accumulators; error vs oracle at the fp32-MFMA "
              "path's level, tests/test_gpu_parity.py)",
@@ -486,13 +489,12 @@ def main():
             # kernel instantiation for every layer (CATEARS_X6_F32IN=0: the
             # plane-operand kernels, hidden layers in their split-output form)
             f32in = split == "bf16x6" and os.environ.get("CATEARS_X6_F32IN", "1") != "0"
-            kname = SPLIT_ROOFLINE_KERNEL[split] if f32in or split != "bf16x6" else \
-                "gemm_bf16x6q_kernel<catears::X6Cfg<128, 128, 4, 2, 3>, true, 0>"
+            kname = SPLIT_ROOFLINE_KERNEL[split if f32in or split != "bf16x6" else "bf16x6p"]
             traffic, src = pmc_traffic(kname)
-            eb = 4 if f32in else {"bf16x6": 6, "f16x3": 4}[split]
+            eb = 4 if f32in else {"bf16x6": 6, "bf16x6p": 6, "f16x3": 4}[split]
             roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1),
                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                        "peak_basis": f"{'bf16' if split == 'bf16x6' else 'fp16'} dense MFMA "
+                        "peak_basis": f"{'fp16' if split == 'f16x3' else 'bf16'} dense MFMA "
                                       f"{MFMA_BF16_PEAK_TFLOPS:g} TFLOP/s / {prods} MFMA products per fp32 "
                                       "multiply-add (achieved = fp32 algorithmic FLOPs)",
                         "mfma_16bit_tflops": round(achieved * prods, 1),

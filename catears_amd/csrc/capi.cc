@@ -373,6 +373,7 @@ static int default_gemm() {
     if (e && !strcmp(e, "fp32")) return (int)CE_GPU_GEMM_FP32;
     if (e && !strcmp(e, "bf16x6")) return (int)CE_GPU_GEMM_BF16X6;
     if (e && !strcmp(e, "f16x3")) return (int)CE_GPU_GEMM_F16X3;
+    if (e && !strcmp(e, "bf16x6p")) return (int)CE_GPU_GEMM_BF16X6_PLANES;
     return (int)CE_GPU_GEMM_BF16X6;
   }();
   return g;
@@ -516,6 +517,7 @@ static int build_program(const std::vector<RawLayer> &layers, int left, int righ
   m->x3_ok = m->x3_ok && m->x6_ok;
   const int want = default_gemm();
   m->gemm = want == CE_GPU_GEMM_F16X3 && m->x3_ok   ? CE_GPU_GEMM_F16X3
+            : want == CE_GPU_GEMM_BF16X6_PLANES && m->x6_ok ? CE_GPU_GEMM_BF16X6_PLANES
             : want != CE_GPU_GEMM_FP32 && m->x6_ok ? CE_GPU_GEMM_BF16X6
                                                     : CE_GPU_GEMM_FP32;
   return CE_GPU_OK;
@@ -789,7 +791,8 @@ int ce_gpu_model_info(const ce_gpu_model *m, int *left_context, int *right_conte
 
 int ce_gpu_model_set_gemm(ce_gpu_model *m, int mode) {
   if (!m) return fail(CE_GPU_EINVAL, "NULL model");
-  if (mode != CE_GPU_GEMM_FP32 && mode != CE_GPU_GEMM_BF16X6 && mode != CE_GPU_GEMM_F16X3)
+  if (mode != CE_GPU_GEMM_FP32 && mode != CE_GPU_GEMM_BF16X6 && mode != CE_GPU_GEMM_F16X3 &&
+      mode != CE_GPU_GEMM_BF16X6_PLANES)
     return fail(CE_GPU_EINVAL, "unknown GEMM mode");
   if (mode != CE_GPU_GEMM_FP32 && !m->x6_ok)
     return fail(CE_GPU_ENOTSUP, "this nnet program cannot run on split planes (unfused row op or widths)");
@@ -1303,6 +1306,7 @@ static int run_steps(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, int
                      const int *row_map, const uint32_t *row_edge, const float **y, int *ldy) {
   if (m->int8) return run_steps_i8(ctx, m, x, ldx, rows, row_map, row_edge, y, ldy);
   if (m->gemm == CE_GPU_GEMM_F16X3) return run_steps_x3(ctx, m, x, ldx, rows, row_map, y, ldy);
+  if (m->gemm == CE_GPU_GEMM_BF16X6_PLANES) return run_steps_x6(ctx, m, x, ldx, rows, row_map, y, ldy);
   if (m->gemm == CE_GPU_GEMM_BF16X6)
     return x6_f32in() ? run_steps_x6f(ctx, m, x, ldx, rows, row_map, y, ldy)
                       : run_steps_x6(ctx, m, x, ldx, rows, row_map, y, ldy);

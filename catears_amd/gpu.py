@@ -34,7 +34,7 @@ ABI = [
 ]
 
 # ce_gpu_model_set_gemm modes
-GEMM_MODES = {"fp32": 0, "bf16x6": 1, "f16x3": 2}
+GEMM_MODES = {"fp32": 0, "bf16x6": 1, "f16x3": 2, "bf16x6p": 3}
 
 _lib = None
 
@@ -214,8 +214,10 @@ class Model:
 
     def set_gemm(self, mode):
         """Matrix-core form of the fp32 Linear layers: "fp32" (fp32 MFMA),
-        "bf16x6" (three-plane bf16 split, six products) or "f16x3" (two scaled
-        fp16 planes, three products); ce_gpu_model_set_gemm."""
+        "bf16x6" (three-plane bf16 split on the way into LDS, six products),
+        "bf16x6p" (the same with the planes stored in HBM; bit-identical) or
+        "f16x3" (two scaled fp16 planes, three products);
+        ce_gpu_model_set_gemm."""
         check(lib().ce_gpu_model_set_gemm(self.h, GEMM_MODES[mode]))
         return self
 

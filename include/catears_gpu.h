@@ -141,7 +141,8 @@ int ce_gpu_model_quantize(ce_gpu_ctx *ctx, ce_gpu_model *m);
  *                      fp32; the dropped cross terms are < 2^-25 |w x|, below
  *                      one fp32 rounding, so the result is an fp32 GEMM
  *                      (differently ordered sum), on the 16x faster bf16
- *                      matrix cores.
+ *                      matrix cores.  Operands stay fp32 in HBM and are
+ *                      split on their way into LDS.
  *   CE_GPU_GEMM_F16X3  every operand, scaled by a power of two, as two fp16
  *                      planes (22-23 significant bits), three fp16 MFMA
  *                      products in two fp32 accumulators; dropped term
@@ -154,11 +155,15 @@ int ce_gpu_model_quantize(ce_gpu_ctx *ctx, ce_gpu_model *m);
  * Linear's input width after the first a multiple of 32, output widths
  * multiples of 4, every ReLU/BatchNorm fused into a Linear), else FP32.
  * F16X3 (22-23 significant bits per operand, not a full fp32 significand)
- * is opt-in.  Environment CATEARS_NNET_GEMM=fp32|bf16x6|f16x3 overrides the
+ * is opt-in.  Environment CATEARS_NNET_GEMM=fp32|bf16x6|bf16x6p|f16x3 overrides the
  * default.  Setting a mode the model does not allow returns CE_GPU_ENOTSUP. */
 #define CE_GPU_GEMM_FP32 0
 #define CE_GPU_GEMM_BF16X6 1
 #define CE_GPU_GEMM_F16X3 2
+/* BF16X6 with the operands kept as bf16 planes in HBM (each layer's
+ * epilogue writes its output split; 6 B per element instead of 4).  The same
+ * products in the same order as BF16X6: bit-identical results. */
+#define CE_GPU_GEMM_BF16X6_PLANES 3
 int ce_gpu_model_set_gemm(ce_gpu_model *m, int mode);
 int ce_gpu_model_get_gemm(const ce_gpu_model *m, int *mode);
 

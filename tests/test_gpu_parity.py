@@ -145,7 +145,7 @@ def am_oracle(oracle, am, feats, gemm=None):
     return oracle.am_stream(am, feats, chunk_size=am["chunk"], gemm=gemm)
 
 
-@pytest.mark.parametrize("gemm", ["fp32", "bf16x6", "f16x3"])
+@pytest.mark.parametrize("gemm", ["fp32", "bf16x6", "bf16x6p", "f16x3"])
 def test_am_xs_vs_oracle(torch, G, ctx, oracle, xs_config, gemm):
     from catears_amd import formats, synth
     am = formats.read_am(xs_config)
@@ -168,7 +168,7 @@ def test_am_xs_vs_oracle(torch, G, ctx, oracle, xs_config, gemm):
             assert np.abs(o[off[u]:off[u + 1]] - ref).max() <= LOGLIK_TOL, f"utt {u}"
 
 
-@pytest.mark.parametrize("gemm", ["fp32", "bf16x6", "f16x3"])
+@pytest.mark.parametrize("gemm", ["fp32", "bf16x6", "bf16x6p", "f16x3"])
 def test_am_segmentation_is_exact(torch, G, ctx, oracle, xs_config, gemm):
     """Splitting an utterance over chunks (max_rows) must not change a bit:
     every output element is the same k-ordered MFMA chain whatever the row's
@@ -187,7 +187,7 @@ def test_am_segmentation_is_exact(torch, G, ctx, oracle, xs_config, gemm):
     assert np.array_equal(bits(outs[0]), bits(outs[2]))
 
 
-@pytest.mark.parametrize("gemm", ["fp32", "bf16x6", "f16x3"])
+@pytest.mark.parametrize("gemm", ["fp32", "bf16x6", "bf16x6p", "f16x3"])
 def test_am_s_vs_oracle(torch, G, ctx, oracle, s_config, gemm):
     """Benchmark model (TDNN-S, 34.75 MFLOP/frame) on two utterances; the
     oracle's GEMM is numpy fp32 here for speed (any fp32 summation order is
@@ -307,6 +307,25 @@ def test_quantize_and_u8_gemm_bitexact(torch, G, ctx, oracle, shape):
     assert np.array_equal(got_i, ref_i)
     got_f = G.gemm_u8(ctx, qa, pa, qb, pb).cpu().numpy()
     assert np.array_equal(bits(got_f), bits(oracle.gemm_u8u8f32(oa, sa, za, ob, sb, zb)))
+
+
+def test_bf16x6_plane_and_fp32_operand_kernels_agree_bitwise(torch, G, ctx, oracle, s_config):
+    """CE_GPU_GEMM_BF16X6 (fp32 operands split on the way into LDS) and
+    CE_GPU_GEMM_BF16X6_PLANES (planes written by each epilogue, read from
+    HBM) form the same six products per element in the same order: the
+    log-likelihoods must agree bit for bit (ragged utterances, several
+    chunks)."""
+    from catears_amd import synth
+    fb = oracle.Fbank()
+    lens = [64000, 17777, 48000]
+    feats = [fb.compute(synth.pcm(540 + i, n)) for i, n in enumerate(lens)]
+    x = dev(torch, np.concatenate(feats))
+    outs = []
+    for gemm in ("bf16x6", "bf16x6p"):
+        model = G.Model(ctx, s_config).set_gemm(gemm)
+        plan = G.Plan(ctx, lens, model, max_rows=2048)
+        outs.append(G.am_forward(ctx, model, plan, x).cpu().numpy())
+    assert np.array_equal(bits(outs[0]), bits(outs[1]))
 
 
 def test_f16x3_overflow_is_flagged(torch, G, ctx, xs_config):
