@@ -131,7 +131,12 @@ __device__ __forceinline__ float apply_post(float y, float sc, float of, const i
   if (MODE == kPostModeReluBn) return bn(relu(y));
   if (MODE == kPostModeBnRelu) return relu(bn(y));
   if (MODE == kPostModeGeneric) {
-    for (int q = 0; q < npost; ++q) y = post[q] == kPostRelu ? relu(y) : post[q] == kPostBatchNorm ? bn(y) : y;
+    // static indices (unrolled to the 4-op maximum): a runtime index into the
+    // kernel argument's array would force the whole argument struct into
+    // scratch memory
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (q < npost) y = post[q] == kPostRelu ? relu(y) : post[q] == kPostBatchNorm ? bn(y) : y;
   }
   return y;
 }

@@ -94,6 +94,28 @@ __device__ __forceinline__ void split3(float v, uint16_t *h, uint16_t *m, uint16
   *l = bf16_bits((__bf16)r2);
 }
 
+// split3 for two values at once, packed (low half = a): one
+// v_cvt_pk_bf16_f32 per plane, the bf16 -> f32 widenings as a shift / mask.
+// Bit-identical to split3 on each value (the same RNE conversions and exact
+// subtractions).
+struct Planes2 {
+  uint32_t h, m, l;
+};
+__device__ __forceinline__ Planes2 split3_pair(float a, float b) {
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  auto cvt = [](float x, float y) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){x, y}, bf16x2));
+  };
+  auto lo = [](uint32_t u) { return __builtin_bit_cast(float, u << 16); };
+  auto hi = [](uint32_t u) { return __builtin_bit_cast(float, u & 0xffff0000u); };
+  const uint32_t p0 = cvt(a, b);
+  const float ra = a - lo(p0), rb = b - hi(p0);
+  const uint32_t p1 = cvt(ra, rb);
+  const float sa = ra - lo(p1), sb = rb - hi(p1);
+  return Planes2{p0, p1, cvt(sa, sb)};
+}
+
 template <int BW_, int BF_, int WGW_, int WGF_, int STAGES_>
 struct X6Cfg {
   static constexpr int BW = BW_, BF = BF_, WGW = WGW_, WGF = WGF_, STAGES = STAGES_;
@@ -711,7 +733,7 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6z_kernel(X6Args p) {
 //        drained before step kt's barrier; step kt+1 reads after it.
 // Tiles past the end are clamped to the last one (written to a stage no
 // later step reads), so the body is one basic block.
-template <class C>
+template <class C, int SCHED>
 __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
   constexpr int BW = C::BW, BF = C::BF, TW = C::TW, TF = C::TF, NT = C::NT, STAGE = C::STAGE;
   constexpr int RPP = NT / 4;  // rows per pass (4 threads x 32 B per row)
@@ -757,21 +779,12 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
   };
   // 8 floats -> three 16-B plane chunks at row r of the plane block `base`
   auto put = [&](char *base, int nrows, int r, f32x4v v0, f32x4v v1) {
-    u32x4 h, m, l;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      uint16_t h0, m0, l0, h1, m1, l1;
-      const f32x4v &v = e < 2 ? v0 : v1;
-      split3(v[(2 * e) & 3], &h0, &m0, &l0);
-      split3(v[(2 * e + 1) & 3], &h1, &m1, &l1);
-      h[e] = h0 | ((uint32_t)h1 << 16);
-      m[e] = m0 | ((uint32_t)m1 << 16);
-      l[e] = l0 | ((uint32_t)l1 << 16);
-    }
+    const Planes2 q0 = split3_pair(v0.x, v0.y), q1 = split3_pair(v0.z, v0.w);
+    const Planes2 q2 = split3_pair(v1.x, v1.y), q3 = split3_pair(v1.z, v1.w);
     const int off = r * 64 + ((pch ^ swz(r)) * 16);
-    *reinterpret_cast<u32x4 *>(base + off) = h;
-    *reinterpret_cast<u32x4 *>(base + nrows * 64 + off) = m;
-    *reinterpret_cast<u32x4 *>(base + 2 * nrows * 64 + off) = l;
+    *reinterpret_cast<u32x4 *>(base + off) = u32x4{q0.h, q1.h, q2.h, q3.h};
+    *reinterpret_cast<u32x4 *>(base + nrows * 64 + off) = u32x4{q0.m, q1.m, q2.m, q3.m};
+    *reinterpret_cast<u32x4 *>(base + 2 * nrows * 64 + off) = u32x4{q0.l, q1.l, q2.l, q3.l};
   };
   auto store = [&](int kt) {
     char *st = smem + (kt & 1) * STAGE;
@@ -827,6 +840,22 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[2][j], acc[i][j], 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2][i], b[0][j], acc[i][j], 0, 0, 0);
       }
+    if constexpr (SCHED == 1) {
+      // interleave: plane-0 fragment reads first, then one MFMA per step
+      // with two VALU (the split of tile kt+1) and the remaining fragment
+      // reads / plane writes / next loads spread between the MFMAs
+      constexpr int NFR = TW + TF, NMM = 6 * TW * TF;
+      __builtin_amdgcn_sched_group_barrier(0x100, NFR, 0);
+#pragma unroll
+      for (int g = 0; g < NMM / 2; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+        if (g < 2 * NFR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        else if (g < 2 * NFR + 3 * (NPW + NPX)) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+        else if (g < 2 * NFR + 3 * (NPW + NPX) + 2 * (NPW + NPX)) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, NMM / 2, 0);
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
@@ -1043,12 +1072,12 @@ int launch_z(hipStream_t s, X6Args p, bool out16) {
   return CE_GPU_OK;
 }
 
-template <class C>
+template <class C, int SCHED = 0>
 int launch_f(hipStream_t s, X6Args p) {
   p.tiles_n = (p.n + C::BW - 1) / C::BW;
   p.tiles_m = (p.m + C::BF - 1) / C::BF;
   dim3 grid(p.tiles_m * p.tiles_n), block(C::NT);
-  hipLaunchKernelGGL((gemm_bf16x6f_kernel<C>), grid, block, 0, s, p);
+  hipLaunchKernelGGL((gemm_bf16x6f_kernel<C, SCHED>), grid, block, 0, s, p);
   CE_HIP(hipGetLastError());
   return CE_GPU_OK;
 }
@@ -1133,6 +1162,10 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
         return launch_f<X6Cfg<128, 128, 2, 4, 2>>(s, p);
       case 43:
         return launch_f<X6Cfg<256, 128, 4, 2, 2>>(s, p);
+      case 44:
+        return launch_f<X6Cfg<128, 256, 2, 4, 2>, 1>(s, p);
+      case 45:
+        return launch_f<X6Cfg<256, 128, 4, 2, 2>, 1>(s, p);
       default:  // = 42
         return launch_f<X6Cfg<128, 256, 2, 4, 2>>(s, p);
     }
