@@ -371,6 +371,7 @@ def main():
     done = [None] * nbuf  # event: the batch that last wrote outs[o] has finished
     gather = world > 1 and not args.no_gather
     gat = LoglikGather(outs[0].shape, torch.float32, "cuda", depth=nbuf) if gather else None
+    comm = torch.cuda.Stream() if gather else None
     checksum = torch.zeros((), dtype=torch.float64, device="cuda")
 
     def front_stage(i):
@@ -387,10 +388,10 @@ def main():
         slot, o, b = i % F, i % nbuf, i % NB
         stream = backs[b]
         if gat is not None:
-            gat.wait_slot(o)  # the gather from nbuf steps ago has read outs[o]
-            # the collective runs on the default (first) stream: order the write after it
-            if b:
-                stream.wait_stream(backs[0])
+            # the gather from nbuf steps ago has read outs[o]: only this
+            # stream waits for it (work.wait() orders the current stream)
+            with torch.cuda.stream(stream):
+                gat.wait_slot(o)
         if done[o] is not None:
             stream.wait_event(done[o])  # the batch nbuf steps ago (maybe another stream) wrote outs[o]
         stream.wait_event(ready[slot])
@@ -400,8 +401,12 @@ def main():
         ev.record(stream)
         done[o] = ev
         if gat is not None:
-            backs[0].wait_event(ev)
-            assert gat.submit(outs[o]) == o
+            # the collective is enqueued from a stream of its own that waits
+            # for this batch only, so the nnet streams never wait on each
+            # other through it
+            with torch.cuda.stream(comm):
+                comm.wait_event(ev)
+                assert gat.submit(outs[o]) == o
 
     def run(first, count):
         front_stage(first)

@@ -50,7 +50,9 @@ class LoglikGather:
         if self.rank == 0:
             self.recv = [[torch.empty(shape, dtype=dtype, device=device) for _ in range(self.world)]
                          for _ in range(depth)]
-        self.checksum = torch.zeros((), dtype=torch.float64, device=device)
+        # one accumulator per slot: a slot's retirements are ordered through
+        # its gathers even when callers retire slots from different streams
+        self.sums = [torch.zeros((), dtype=torch.float64, device=device) for _ in range(depth)]
         self.batches = 0
         self.slot = 0
 
@@ -62,7 +64,7 @@ class LoglikGather:
         self.pending[s] = None
         if self.rank == 0:
             for t in self.recv[s]:
-                self.checksum += t[0].double().sum()
+                self.sums[s] += t[0].double().sum()
         self.batches += 1
 
     def submit(self, t):
@@ -73,8 +75,14 @@ class LoglikGather:
         self.slot = (s + 1) % self.depth
         return s
 
+    @property
+    def checksum(self):
+        return sum(self.sums[1:], self.sums[0].clone())
+
     def wait_slot(self, s):
-        """Block until the gather occupying slot s has read its input."""
+        """Order the current stream after the gather occupying slot s (NCCL:
+        a stream wait; gloo: the host blocks) -- after it, that gather's
+        input may be overwritten."""
         self._retire(s)
 
     def drain(self):
