@@ -840,6 +840,16 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[2][j], acc[i][j], 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2][i], b[0][j], acc[i][j], 0, 0, 0);
       }
+    if constexpr (SCHED == 2) {
+      // all fragment reads of stage kt first, so their latency hides under
+      // the split of tile kt+1 (VALU + plane writes) and the next loads;
+      // then the MFMAs
+      __builtin_amdgcn_sched_group_barrier(0x100, 3 * (TW + TF), 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 512, 0);
+      __builtin_amdgcn_sched_group_barrier(0x200, 3 * (NPW + NPX), 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 2 * (NPW + NPX), 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 6 * TW * TF, 0);
+    }
     if constexpr (SCHED == 1) {
       // interleave: plane-0 fragment reads first, then one MFMA per step
       // with two VALU (the split of tile kt+1) and the remaining fragment
@@ -1166,6 +1176,10 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
         return launch_f<X6Cfg<128, 256, 2, 4, 2>, 1>(s, p);
       case 45:
         return launch_f<X6Cfg<256, 128, 4, 2, 2>, 1>(s, p);
+      case 46:
+        return launch_f<X6Cfg<128, 256, 2, 4, 2>, 2>(s, p);
+      case 47:
+        return launch_f<X6Cfg<256, 128, 4, 2, 2>, 2>(s, p);
       default:  // = 42
         return launch_f<X6Cfg<128, 256, 2, 4, 2>>(s, p);
     }
