@@ -56,11 +56,10 @@ struct WaveSmem {
 };
 
 // Tables staged once per block in LDS (indexed by generation / band at run
-// time): each lane op's descriptor (slots, kind, twiddles) and mel weights.
+// time): each lane op's twiddles and the mel weights (the op's slots and
+// kind live in the lane's registers).
 struct BlockTables {
   float tw[kFftGens * 64 * 6];  // each lane op's six twiddles
-  uint32_t addr[kFftGens * 64];
-  uint32_t meta[kFftGens * 64];
   float mel_w[512];
 };
 
@@ -81,7 +80,6 @@ __global__ __launch_bounds__(256) void fbank_kernel(const FbankTables *__restric
   __shared__ BlockTables bt;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (int i = threadIdx.x; i < kFftGens * 64 * 6; i += 256) bt.tw[i] = tab->fft_tw[i];
-  for (int i = threadIdx.x; i < kFftGens * 64; i += 256) bt.addr[i] = tab->fft_addr[i], bt.meta[i] = tab->fft_meta[i];
   for (int i = threadIdx.x; i < 512; i += 256) bt.mel_w[i] = tab->mel_w[i];
   float win[7];
 #pragma unroll
@@ -94,6 +92,15 @@ __global__ __launch_bounds__(256) void fbank_kernel(const FbankTables *__restric
   const float kn1r = tab->kn[2 * k1], kn1i = tab->kn[2 * k1 + 1];
   const int a0 = fb::sw(fb::bitrev8(k0)), b0 = fb::sw(fb::bitrev8(256 - k0));
   const int a1 = fb::sw(fb::bitrev8(k1)), b1 = fb::sw(fb::bitrev8((256 - k1) & 255));
+  // this lane's FFT op slots and kinds for every generation, in registers
+  // (the frame loop then needs no descriptor load before its LDS accesses)
+  uint32_t gaddr[kFftGens];
+  uint32_t gmeta = 0;
+#pragma unroll
+  for (int g = 0; g < kFftGens; ++g) {
+    gaddr[g] = tab->fft_addr[g * 64 + lane];
+    gmeta |= (tab->fft_meta[g * 64 + lane] & 15u) << (4 * g);
+  }
   const int band = lane < kMel ? lane : 0;
   const int mel_off = tab->mel_off[band], mel_len = lane < kMel ? tab->mel_len[band] : 0;
   const int mel_wbase = tab->mel_wbase[band];
@@ -143,11 +150,18 @@ __global__ __launch_bounds__(256) void fbank_kernel(const FbankTables *__restric
     }
     wave_sync();
 
-    // 3. split-radix generations
+    // 3. split-radix generations (the descriptors rotate through the
+    // registers: after kFftGens steps they are back in place for the next
+    // frame, and the loop stays rolled, keeping the register count low)
 #pragma unroll 1
     for (int g = 0; g < FBANK_GENS; ++g) {
       const int o = g * 64 + lane;
-      fb::fft_lane_op(bt.addr[o], bt.meta[o], bt.tw + 6 * o, S.re, S.im);
+      fb::fft_lane_op(gaddr[0], gmeta & 15u, bt.tw + 6 * o, S.re, S.im);
+      const uint32_t a0 = gaddr[0];
+#pragma unroll
+      for (int j = 0; j + 1 < kFftGens; ++j) gaddr[j] = gaddr[j + 1];
+      gaddr[kFftGens - 1] = a0;
+      gmeta = (gmeta >> 4) | ((gmeta & 15u) << (4 * (kFftGens - 1)));
       wave_sync();
     }
 
