@@ -167,8 +167,10 @@ __device__ __forceinline__ void x6_epilogue(const X6Args &p, const f32x4 (&acc)[
   });
 }
 
-// DIAG (tuning builds only, wrong results): 1 = DMAs and fragment reads
-// without the MFMAs, 2 = fragment reads and MFMAs without the DMAs.
+// DIAG (ablation builds, wrong results; not dispatched by the library -- the
+// measurements they gave are recorded in DESIGN.md §8): 1 = DMAs and
+// fragment reads without the MFMAs, 2 = fragment reads and MFMAs without the
+// DMAs, 3/4 = DMA shape / L2-resident-tile ablations.
 template <class C, bool OUT16, int DIAG = 0>
 __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6_kernel(X6Args p) {
   constexpr int BW = C::BW, BF = C::BF, TW = C::TW, TF = C::TF;
@@ -1211,28 +1213,10 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
       return launch_phased<X6Cfg<64, 128, 2, 2, 3>>(s, p, out16);
     case 93:
       return launch_cfg<X6Cfg<128, 128, 2, 4, 3>>(s, p, out16);
-    case 94:  // tuning only
-      return launch_cfg<X6Cfg<128, 128, 2, 4, 3>, 1>(s, p, out16);
     case 95:
       return launch_cfg<X6Cfg<256, 128, 4, 2, 2>>(s, p, out16);
-    case 96:  // tuning only
-      return launch_cfg<X6Cfg<256, 128, 4, 2, 2>, 1>(s, p, out16);
     case 97:
       return launch_cfg<X6Cfg<128, 256, 2, 4, 2>>(s, p, out16);
-    case 98:  // tuning only
-      return launch_cfg<X6Cfg<128, 256, 2, 4, 2>, 1>(s, p, out16);
-    case 99:  // tuning only: DMAs as 8 rows x 128 B + fragment reads, no MFMA (wrong results)
-      return launch_cfg<X6Cfg<128, 128, 2, 4, 2>, 3>(s, p, out16);
-    case 100:  // tuning only: as 99 with three stages
-      return launch_cfg<X6Cfg<128, 128, 2, 4, 3>, 3>(s, p, out16);
-    case 101:  // tuning only: as 99, every block on tile (0, 0)
-      return launch_cfg<X6Cfg<128, 128, 2, 4, 2>, 4>(s, p, out16);
-    case 102:  // tuning only: as 100, every block on tile (0, 0)
-      return launch_cfg<X6Cfg<128, 128, 2, 4, 3>, 4>(s, p, out16);
-    case 91:  // tuning only: DMAs + fragment reads, no MFMA (wrong results)
-      return launch_cfg<X6Cfg<128, 128, 2, 4, 2>, 1>(s, p, out16);
-    case 92:  // tuning only: fragment reads + MFMA, no DMA (wrong results)
-      return launch_cfg<X6Cfg<128, 128, 2, 4, 2>, 2>(s, p, out16);
     case 14:
       return launch_reg<X6Cfg<128, 128, 2, 4, 2>>(s, p, out16);
     case 15:
