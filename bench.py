@@ -45,8 +45,8 @@ METRIC = "acoustic frames/sec (fbank->nnet posteriors), 16kHz, 1/2/4/8 GPU"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)  # 0.15 s of GPU time at C3: steady state
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--utts-per-step", type=int, default=None, help="default 4 (c3), 8 (c5)")
     ap.add_argument("--pool", type=int, default=32, help="distinct utterances resident per rank")
     ap.add_argument("--seconds", type=float, default=10.0)
