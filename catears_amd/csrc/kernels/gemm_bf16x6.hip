@@ -1180,6 +1180,10 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
         return launch_f<X6Cfg<256, 128, 4, 2, 2>, 1>(s, p);
       case 46:
         return launch_f<X6Cfg<128, 256, 2, 4, 2>, 2>(s, p);
+      case 48:  // 4 waves of 128 x 64
+        return launch_f<X6Cfg<256, 128, 2, 2, 2>>(s, p);
+      case 49:  // 4 waves of 64 x 128
+        return launch_f<X6Cfg<128, 256, 2, 2, 2>>(s, p);
       case 47:
         return launch_f<X6Cfg<256, 128, 4, 2, 2>, 2>(s, p);
       default:  // = 42
