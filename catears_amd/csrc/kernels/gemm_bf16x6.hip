@@ -823,6 +823,7 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
       for (int j = 0; j < TF; ++j)
         b[pl][j] = *reinterpret_cast<const bf16x8 *>(st + 3 * BW * 64 + (pl * BF + frow + j * 16) * 64 + foff);
     }
+    if constexpr (SCHED == 3) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < TW; ++i)
 #pragma unroll
@@ -842,6 +843,7 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[2][j], acc[i][j], 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2][i], b[0][j], acc[i][j], 0, 0, 0);
       }
+    if constexpr (SCHED == 3) __builtin_amdgcn_s_setprio(0);
     if constexpr (SCHED == 2) {
       // all fragment reads of stage kt first, so their latency hides under
       // the split of tile kt+1 (VALU + plane writes) and the next loads;
@@ -1180,6 +1182,8 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
         return launch_f<X6Cfg<256, 128, 4, 2, 2>, 1>(s, p);
       case 46:
         return launch_f<X6Cfg<128, 256, 2, 4, 2>, 2>(s, p);
+      case 50:  // raised priority around the MFMAs
+        return launch_f<X6Cfg<128, 256, 2, 4, 2>, 3>(s, p);
       case 48:  // 4 waves of 128 x 64
         return launch_f<X6Cfg<256, 128, 2, 2, 2>>(s, p);
       case 49:  // 4 waves of 64 x 128
