@@ -248,6 +248,32 @@ def test_score_pipeline_with_cmvn(torch, G, ctx, oracle, xs_config, global_stats
         assert np.abs(out[off[u]:off[u + 1]] - ref).max() <= LOGLIK_TOL
 
 
+def test_c3_full_batch_vs_oracle(torch, G, ctx, oracle, s_config):
+    """The benchmark's own step at full size: four 10 s utterances packed
+    into one 4072-row chunk, fbank -> CMVN (synthetic global stats, as
+    bench.py) -> TDNN-S in the default GEMM mode -> minus log prior, against
+    the oracle (fbank / CMVN restatement in C, the network in fp64) within the
+    north star's 1e-4 on every log-likelihood."""
+    from catears_amd import formats, synth
+    am = formats.read_am(s_config)
+    model = G.Model(ctx, s_config)
+    n = 160000
+    waves = [synth.pcm(i, n) for i in range(4)]  # bench.py's rank-0 pool seeds
+    gstats = synth.cmvn_stats_synthetic()
+    plan = G.Plan(ctx, [n] * 4, model)
+    assert plan.total_frames == 4 * 998
+    out = G.score(ctx, model, plan, dev(torch, np.concatenate(waves)), dev(torch, gstats)).cpu().numpy()
+    off = plan.frame_offsets
+    fb = oracle.Fbank()
+    f64 = lambda a, w: (a.astype(np.float64) @ w.astype(np.float64)).astype(np.float32)
+    worst = 0.0
+    for u, w in enumerate(waves):
+        ref = oracle.am_whole(am, oracle.cmvn(gstats, fb.compute(w)), gemm=f64)
+        worst = max(worst, float(np.abs(out[off[u]:off[u + 1]] - ref).max()))
+    assert np.isfinite(out).all()
+    assert worst <= LOGLIK_TOL, worst
+
+
 def test_model_rejects_bad_topology(torch, G, ctx, tmp_path):
     from catears_amd import formats
     W = np.ones((40, 8), np.float32)
