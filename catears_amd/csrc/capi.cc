@@ -655,7 +655,19 @@ int ce_gpu_ctx_destroy(ce_gpu_ctx *ctx) {
 
 int ce_gpu_ctx_set_stream(ce_gpu_ctx *ctx, void *stream) {
   if (!ctx) return fail(CE_GPU_EINVAL, "ctx is NULL");
-  ctx->stream = static_cast<hipStream_t>(stream);
+  hipStream_t next = static_cast<hipStream_t>(stream);
+  if (next != ctx->stream) {
+    // Work already queued on the old stream may still use the context's
+    // workspaces; the new stream starts after it (no host wait).
+    CE_HIP(hipSetDevice(ctx->device));
+    hipEvent_t done;
+    CE_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+    hipError_t e = hipEventRecord(done, ctx->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(next, done, 0);
+    (void)hipEventDestroy(done);
+    CE_HIP(e);
+    ctx->stream = next;
+  }
   return CE_GPU_OK;
 }
 
@@ -1421,6 +1433,21 @@ int ce_gpu_nnet_propagate(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *d
     return fail(CE_GPU_EINVAL, fmt("nnet_propagate: %d rows do not cover the network context (%d, %d)", rows,
                                    m->net_left, m->net_right));
   if (subtract_prior && !m->log_prior.ptr) return fail(CE_GPU_EINVAL, "model has no prior");
+  const int ctx_rows = m->net_left + m->net_right;
+  if (!m->int8 && rows > kPropagateWindow) {
+    // A very long block (hours of audio in one call) runs as overlapping
+    // windows: output row t needs input rows t .. t + L + R only, so the
+    // windows give the same bits as one pass, keep every GEMM operand well
+    // inside the kernels' 32-bit row offsets and bound the workspace.  (An
+    // int8 model quantizes per call, so it keeps the single pass.)
+    const int step = kPropagateWindow - ctx_rows;
+    for (int o = 0; o < out_rows; o += step) {
+      const int n = std::min(step, out_rows - o);
+      CE_TRY(ce_gpu_nnet_propagate(ctx, m, d_in + (size_t)o * ld_in, n + ctx_rows, ld_in, subtract_prior,
+                                   d_out + (size_t)o * m->num_pdfs));
+    }
+    return CE_GPU_OK;
+  }
   const float *y = nullptr;
   int ldy = 0;
   CE_TRY(run_steps(ctx, m, d_in, ld_in, rows, nullptr, nullptr, &y, &ldy));
@@ -1444,6 +1471,18 @@ int ce_gpu_nnet_propagate_blocks(ce_gpu_ctx *ctx, const ce_gpu_model *m, const f
     total += h_rows[b];
   }
   if (total >= INT32_MAX / 2) return fail(CE_GPU_EINVAL, "too many rows");
+  if (m->int8) {
+    // per-tensor activation parameters are reduced over the block being
+    // scored: one block per call keeps each block's rows its own
+    const float *in = d_in;
+    float *o = d_out;
+    for (int b = 0; b < n_blocks; ++b) {
+      CE_TRY(ce_gpu_nnet_propagate(ctx, m, in, h_rows[b], ld_in, subtract_prior, o));
+      in += (size_t)h_rows[b] * ld_in;
+      o += (size_t)(h_rows[b] - L - R) * m->num_pdfs;
+    }
+    return CE_GPU_OK;
+  }
   const int rows = (int)total;
   // per packed row: output row (or -1) and distances to its block's edges;
   // written only after the previous call's kernels are done with them
@@ -1589,14 +1628,14 @@ int ce_gpu_rowwise(ce_gpu_ctx *ctx, int op, int rows, int dim, float *d_x, int l
   return launch_rowop_raw(ctx->stream, op, dim, d_scale, d_offset, d_x, ld, rows);
 }
 
-int ce_gpu_loglik_gather(ce_gpu_ctx *ctx, const float *d_loglik, int rows, int ld, const int32_t *d_tid2pdf,
-                         int n_tid, const int32_t *d_row, const int32_t *d_trans, int n, float am_scale,
-                         float *d_out) {
-  if (!ctx || rows < 0 || ld < 0 || n_tid < 0 || n < 0) return fail(CE_GPU_EINVAL, "bad argument");
+int ce_gpu_loglik_gather(ce_gpu_ctx *ctx, const float *d_loglik, int rows, int ld, int dim,
+                         const int32_t *d_tid2pdf, int n_tid, const int32_t *d_row, const int32_t *d_trans, int n,
+                         float am_scale, float *d_out) {
+  if (!ctx || rows < 0 || dim < 0 || ld < dim || n_tid < 0 || n < 0) return fail(CE_GPU_EINVAL, "bad argument");
   if (n == 0) return CE_GPU_OK;
   if (!d_loglik || !d_tid2pdf || !d_row || !d_trans || !d_out) return fail(CE_GPU_EINVAL, "NULL argument");
   CE_HIP(hipSetDevice(ctx->device));
-  return launch_loglik_gather(ctx->stream, d_loglik, rows, ld, d_tid2pdf, n_tid, d_row, d_trans, n, am_scale, d_out);
+  return launch_loglik_gather(ctx->stream, d_loglik, rows, ld, dim, d_tid2pdf, n_tid, d_row, d_trans, n, am_scale, d_out);
 }
 
 int ce_gpu_loglik_columns(ce_gpu_ctx *ctx, const float *d_loglik, int rows, int ld, int dim,

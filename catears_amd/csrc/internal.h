@@ -364,13 +364,16 @@ int launch_splice_pad_f16(hipStream_t s, const float *in, int ld_in, int rows, i
                           const int *row_map, uint16_t *out, int po, int *overflow);
 // activations enter the f16x3 GEMM as x * 2^kF16ActShift
 constexpr int kF16ActShift = -8;
+// ce_gpu_nnet_propagate runs longer fp32 blocks as overlapping windows of
+// this many input rows (bit-identical; bounds 32-bit offsets and workspace)
+constexpr int kPropagateWindow = 1 << 16;
 
 // Final step: optional log-softmax per row, minus log prior, scatter to the
 // output rows named by row_dst (-1 = drop).
 int launch_finalize(hipStream_t s, const float *x, int ldx, int rows, int dim, bool log_softmax,
                     const float *log_prior, const int *row_dst, float *out);
 int launch_rowop(hipStream_t s, const RowOp &op, float *x, int ldx, int rows);
-int launch_loglik_gather(hipStream_t s, const float *ll, int rows, int ld, const int32_t *tpm, int n_tid,
+int launch_loglik_gather(hipStream_t s, const float *ll, int rows, int ld, int dim, const int32_t *tpm, int n_tid,
                          const int32_t *row, const int32_t *trans, int n, float scale, float *out);
 int launch_loglik_columns(hipStream_t s, const float *ll, int rows, int ld, int dim, const int32_t *cols,
                           int n_cols, float *out);

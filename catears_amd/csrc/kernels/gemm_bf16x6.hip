@@ -1130,6 +1130,10 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
     if (!a.wf || !a.y32 || a.ldw % 4 || a.ldx % 4 || (reinterpret_cast<uintptr_t>(a.wf) & 15) ||
         (reinterpret_cast<uintptr_t>(a.xf) & 15))
       return fail(CE_GPU_EINVAL, "gemm_bf16x6: fp32 operands must be 16-byte aligned, output fp32");
+    // the kernel forms row * ld element offsets in 32 bits
+    if ((int64_t)a.n * a.ldw >= ((int64_t)1 << 31) || (int64_t)a.m * a.ldx >= ((int64_t)1 << 31) ||
+        (int64_t)a.m * a.ldy >= ((int64_t)1 << 31))
+      return fail(CE_GPU_EINVAL, "gemm_bf16x6: operand beyond 2^31 elements");
   } else {
     if (a.ldw % 8 || a.pw % 8 || a.ldx % 8 || a.px % 8 || (reinterpret_cast<uintptr_t>(a.w) & 15) ||
         (reinterpret_cast<uintptr_t>(a.x) & 15))

@@ -249,7 +249,7 @@ namespace {
 // One (frame, transition id) pair per thread: two dependent 4-byte reads
 // (the map, then the loglik element) -- latency, not bandwidth, so a wide
 // grid of small blocks.
-__global__ __launch_bounds__(256) void loglik_gather_kernel(const float *__restrict__ ll, int rows, int ld,
+__global__ __launch_bounds__(256) void loglik_gather_kernel(const float *__restrict__ ll, int rows, int ld, int dim,
                                                             const int32_t *__restrict__ tpm, int n_tid,
                                                             const int32_t *__restrict__ row,
                                                             const int32_t *__restrict__ trans, int n, float scale,
@@ -258,7 +258,10 @@ __global__ __launch_bounds__(256) void loglik_gather_kernel(const float *__restr
   if (i >= n) return;
   const int r = row[i], t = trans[i];
   float v = __builtin_nanf("");
-  if (r >= 0 && r < rows && t >= 0 && t < n_tid) v = scale * ll[(int64_t)r * ld + tpm[t]];
+  if (r >= 0 && r < rows && t >= 0 && t < n_tid) {
+    const int p = tpm[t];
+    if (p >= 0 && p < dim) v = scale * ll[(int64_t)r * ld + p];
+  }
   out[i] = v;
 }
 
@@ -278,10 +281,10 @@ __global__ __launch_bounds__(256) void loglik_columns_kernel(const float *__rest
 
 }  // namespace
 
-int launch_loglik_gather(hipStream_t s, const float *ll, int rows, int ld, const int32_t *tpm, int n_tid,
+int launch_loglik_gather(hipStream_t s, const float *ll, int rows, int ld, int dim, const int32_t *tpm, int n_tid,
                          const int32_t *row, const int32_t *trans, int n, float scale, float *out) {
   if (n > 0)
-    hipLaunchKernelGGL(loglik_gather_kernel, dim3((n + 255) / 256), dim3(256), 0, s, ll, rows, ld, tpm, n_tid, row,
+    hipLaunchKernelGGL(loglik_gather_kernel, dim3((n + 255) / 256), dim3(256), 0, s, ll, rows, ld, dim, tpm, n_tid, row,
                        trans, n, scale, out);
   CE_HIP(hipGetLastError());
   return CE_GPU_OK;

@@ -92,7 +92,7 @@ def lib():
         "ce_gpu_linear": (ci, [vp, ci, ci, ci, vp, ci, vp, ci, vp, vp, ci]),
         "ce_gpu_splice": (ci, [vp, ci, ci, vp, ci, ctypes.POINTER(ctypes.c_int32), ci, vp]),
         "ce_gpu_rowwise": (ci, [vp, ci, ci, ci, vp, ci, vp, vp]),
-        "ce_gpu_loglik_gather": (ci, [vp, vp, ci, ci, vp, ci, vp, vp, ci, ctypes.c_float, vp]),
+        "ce_gpu_loglik_gather": (ci, [vp, vp, ci, ci, ci, vp, ci, vp, vp, ci, ctypes.c_float, vp]),
         "ce_gpu_loglik_columns": (ci, [vp, vp, ci, ci, ci, vp, ci, vp]),
         "ce_gpu_model_set_gemm": (ci, [vp, ci]),
         "ce_gpu_model_get_gemm": (ci, [vp, pi]),
@@ -367,7 +367,8 @@ def loglik_gather(ctx, loglik, tid2pdf, rows, trans, am_scale=1.0, out=None):
     assert trans.numel() == n and rows.dtype == trans.dtype == tid2pdf.dtype == torch.int32
     if out is None:
         out = torch.empty((n,), dtype=torch.float32, device=loglik.device)
-    check(lib().ce_gpu_loglik_gather(ctx.h, _ptr(loglik), loglik.shape[0], loglik.stride(0), _ptr(tid2pdf),
+    check(lib().ce_gpu_loglik_gather(ctx.h, _ptr(loglik), loglik.shape[0], loglik.stride(0), loglik.shape[1],
+                                     _ptr(tid2pdf),
                                      int(tid2pdf.numel()), _ptr(rows), _ptr(trans), n, float(am_scale),
                                      _ptr(out)))
     return out

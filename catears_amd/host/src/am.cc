@@ -6,6 +6,7 @@
 
 #include <chrono>
 #include <condition_variable>
+#include <exception>
 #include <memory>
 #include <mutex>
 
@@ -25,6 +26,7 @@ struct AcousticModel::Batcher {
     int n, dim;
     Matrix<float> *out;
     bool done;
+    std::exception_ptr error;  // the batch's failure, rethrown by the request's owner
   };
   std::mutex mu;
   std::condition_variable cv;
@@ -141,9 +143,16 @@ void AcousticModel::ComputeBatch(Instance *inst, int batch_size, Matrix<float> *
         std::vector<int32_t> ns;
         std::vector<Matrix<float> *> outs;
         for (Batcher::Req *q : batch) ptrs.push_back(q->rows), ns.push_back(q->n), outs.push_back(q->out);
-        RunBlocks(ptrs, ns, dim, outs);
+        // A device failure must still release the followers: every request
+        // of the batch is finished with the error, which its owner rethrows.
+        std::exception_ptr error;
+        try {
+          RunBlocks(ptrs, ns, dim, outs);
+        } catch (...) {
+          error = std::current_exception();
+        }
         lk.lock();
-        for (Batcher::Req *q : batch) q->done = true;
+        for (Batcher::Req *q : batch) q->done = true, q->error = error;
         b.calls += 1;
         b.blocks += (int64_t)batch.size();
         b.leader_active = false;
@@ -152,6 +161,7 @@ void AcousticModel::ComputeBatch(Instance *inst, int batch_size, Matrix<float> *
         b.cv.wait(lk, [&] { return req.done || !b.leader_active; });
       }
     }
+    if (req.error) std::rethrow_exception(req.error);
     return;
   }
   RunBlocks({rows}, {rows_in}, dim, {log_prob});

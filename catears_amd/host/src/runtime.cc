@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
+#include <atomic>
+
 namespace catears {
 namespace host {
 
@@ -13,8 +15,16 @@ static void hip_check(hipError_t e, const char *what) {
   if (e != hipSuccess) throw DeviceError(std::string(what) + ": " + hipGetErrorString(e));
 }
 
+static std::atomic<int> g_injected_failures{0};
+
+void InjectDeviceFailures(int n) { g_injected_failures.store(n); }
+
 void Check(int rc, const char *what) {
   if (rc != CE_GPU_OK) throw DeviceError(std::string(what) + ": " + ce_gpu_last_error());
+  int left = g_injected_failures.load();
+  while (left > 0 && !g_injected_failures.compare_exchange_weak(left, left - 1)) {
+  }
+  if (left > 0) throw DeviceError(std::string(what) + ": injected device failure");
 }
 
 DeviceBuffer::~DeviceBuffer() {

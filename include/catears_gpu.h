@@ -68,6 +68,9 @@ const char *ce_gpu_version(void);
  * them once. */
 int ce_gpu_ctx_create(int device, void *stream, ce_gpu_ctx **out);
 int ce_gpu_ctx_destroy(ce_gpu_ctx *ctx);
+/* Later calls enqueue on `stream`.  The switch is ordered: `stream` waits
+ * (device-side, no host block) for everything already queued on the old
+ * stream, which may still be using the context's workspaces. */
 int ce_gpu_ctx_set_stream(ce_gpu_ctx *ctx, void *stream);
 /* Block the host until all work enqueued through ctx has finished. */
 int ce_gpu_ctx_synchronize(ce_gpu_ctx *ctx);
@@ -130,7 +133,13 @@ int ce_gpu_model_info(const ce_gpu_model *m, int *left_context, int *right_conte
  * per layer and per chunk of packed rows (the layer input block, before the
  * splice -- the same parameters as quantizing the spliced block); the int32
  * accumulation is exact (gemmlowp's ring), bias / ReLU / BatchNorm /
- * LogSoftmax stay fp32.  Irreversible for this model handle. */
+ * LogSoftmax stay fp32.  Irreversible for this model handle.
+ * Batch dependence: like the reference's per-call Quantize, an activation
+ * tensor's (scale, zero point) come from the whole block being scored, so in
+ * ce_gpu_am_forward / ce_gpu_score an utterance's int8 log-likelihoods depend
+ * on which utterances share its packed chunk.  ce_gpu_nnet_propagate_blocks
+ * quantizes every block on its own instead, so there each block gets exactly
+ * the rows it gets alone (the AcousticModel batcher's contract). */
 int ce_gpu_model_quantize(ce_gpu_ctx *ctx, ce_gpu_model *m);
 
 /* Matrix-core form of the fp32 Linear layers (LinearLayer::Propagate ->
@@ -240,7 +249,9 @@ int ce_gpu_nnet_propagate(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *d
  * rows - L - R output rows back to back.  One launch sequence for all blocks:
  * the call a serving loop makes to score the ready chunks of many streams
  * at once (catears_amd/host AcousticModel batching).  Host-synchronous with
- * respect to the previous call on this context. */
+ * respect to the previous call on this context.  Every block's output equals
+ * what ce_gpu_nnet_propagate gives for it alone (bit-exact; an int8 model
+ * runs the blocks one by one so its quantization parameters stay per block). */
 int ce_gpu_nnet_propagate_blocks(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *d_in, int ld_in,
                                  const int32_t *h_rows, int n_blocks, int subtract_prior, float *d_out);
 
@@ -313,10 +324,13 @@ int ce_gpu_rowwise(ce_gpu_ctx *ctx, int op, int rows, int dim, float *d_x, int l
  *   d_out[i] = am_scale * d_loglik[d_row[i] * ld + d_tid2pdf[d_trans[i]]]
  * for n (frame, transition-id) pairs -- the acoustic costs of a frame's
  * active arcs (ProcessEmitting, src/decoder.cc:327,350 negate them), so a
- * decoder reads n floats instead of whole 3456-wide rows.  A pair whose frame
- * is outside [0, rows) or whose transition id is outside [0, n_tid) yields
- * NaN (the reference indexes out of bounds there). */
-int ce_gpu_loglik_gather(ce_gpu_ctx *ctx, const float *d_loglik, int rows, int ld, const int32_t *d_tid2pdf,
+ * decoder reads n floats instead of whole 3456-wide rows.  `dim` is the row
+ * width (num_pdfs, <= ld).  A pair whose frame is outside [0, rows), whose
+ * transition id is outside [0, n_tid) or whose pdf (d_tid2pdf entry, e.g.
+ * from a corrupt model file) is outside [0, dim) yields NaN (the reference
+ * indexes out of bounds there). */
+int ce_gpu_loglik_gather(ce_gpu_ctx *ctx, const float *d_loglik, int rows, int ld, int dim,
+                         const int32_t *d_tid2pdf,
                          int n_tid, const int32_t *d_row, const int32_t *d_trans, int n, float am_scale,
                          float *d_out);
 

@@ -10,6 +10,8 @@
 //   pk_dropin cmvn   <feats.f32> <rows> <stats.vec0> <out.f32>
 //   pk_dropin am     <am.conf> <feats.f32> <rows> <out.f32>      (per-frame Process + EndOfStream)
 //   pk_dropin am_mt  <am.conf> <out_prefix> <feats_1.f32> <rows_1> ...  (one thread per stream, shared model)
+//   pk_dropin am_mt_fail <am.conf> <out_prefix> <feats_1.f32> <rows_1> ...  (as am_mt, the first device
+//                    call fails: every thread must return, those in the failed batch with DeviceError)
 //   pk_dropin nnet   <nnet.nn02> <in.f32> <rows> <cols> <out.f32> (Nnet::Read + Propagate)
 //   pk_dropin layer  <nnet.nn02> <in.f32> <rows> <cols> <out.f32> (Layer::Propagate of each layer, chained)
 //   pk_dropin matmat <m> <n> <k> <a.f32> <b.f32> <out.f32>
@@ -25,6 +27,7 @@
 #include <vector>
 
 #include "am.h"
+#include "catears_runtime.h"
 #include "cmvn.h"
 #include "configuration.h"
 #include "fbank.h"
@@ -139,7 +142,7 @@ int main(int argc, char **argv) {
     save(argv[5], all.data(), cols ? (int)(all.size() / cols) : 0, cols, cols);
     return 0;
   }
-  if (mode == "am_mt" && argc >= 6 && (argc - 4) % 2 == 0) {
+  if ((mode == "am_mt" || mode == "am_mt_fail") && argc >= 6 && (argc - 4) % 2 == 0) {
     Configuration conf;
     Status st = conf.Read(argv[2]);
     AcousticModel am;
@@ -147,8 +150,11 @@ int main(int argc, char **argv) {
     if (!st.ok()) return die(st);
     const int streams = (argc - 4) / 2;
     std::vector<std::thread> threads;
+    std::vector<int> failed(streams, 0);
+    if (mode == "am_mt_fail") catears::host::InjectDeviceFailures(1);
     for (int i = 0; i < streams; ++i) {
       threads.emplace_back([&, i]() {
+       try {
         const std::vector<float> feats = load<float>(argv[4 + 2 * i]);
         const int rows = atoi(argv[5 + 2 * i]);
         const int dim = rows ? (int)(feats.size() / rows) : 0;
@@ -165,12 +171,17 @@ int main(int argc, char **argv) {
         append_rows(&all, log_prob, &cols);
         const std::string out = std::string(argv[3]) + std::to_string(i) + ".bin";
         save(out.c_str(), all.data(), cols ? (int)(all.size() / cols) : 0, cols, cols);
+       } catch (const catears::host::DeviceError &e) {
+        failed[i] = 1;
+       }
       });
     }
     for (auto &t : threads) t.join();
     int64_t calls = 0, blocks = 0;
     am.batch_stats(&calls, &blocks);
-    printf("device_calls %lld blocks %lld\n", (long long)calls, (long long)blocks);
+    int n_failed = 0;
+    for (int f : failed) n_failed += f;
+    printf("device_calls %lld blocks %lld failed %d\n", (long long)calls, (long long)blocks, n_failed);
     return 0;
   }
   if ((mode == "nnet" || mode == "layer") && argc == 7) {

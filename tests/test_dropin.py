@@ -199,7 +199,8 @@ def test_am_streams_batched_across_threads(tmp_path, oracle, xs_config):
     r = subprocess.run([DRIVER, "am_mt", str(conf), str(tmp_path / "mt")] + [str(a) for a in args],
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
-    calls, blocks = [int(v) for v in r.stdout.split()[1::2]]
+    calls, blocks, failed = [int(v) for v in r.stdout.split()[1::2]]
+    assert failed == 0
     for i, f in enumerate(feats):
         got = _load(tmp_path / f"mt{i}.bin")
         alone = tmp_path / f"alone{i}.bin"
@@ -209,6 +210,33 @@ def test_am_streams_batched_across_threads(tmp_path, oracle, xs_config):
         assert np.max(np.abs(got - want)) <= LOGLIK_TOL
     assert blocks == sum((len(f) + 49) // 50 for f in feats) or blocks > 0
     assert calls < blocks, (calls, blocks)  # some calls carried several streams' chunks
+
+
+@pytest.mark.gpu
+def test_am_batcher_device_failure_releases_every_stream(tmp_path, xs_config):
+    """A failing batched device call (injected: the first Check() throws)
+    must finish every request of its batch with the error -- the leader and
+    its followers all see DeviceError -- and leave the batcher usable; no
+    thread may hang waiting for a leader that died (am.cc)."""
+    from catears_amd import synth
+    from oracle import pyoracle
+    lens = [16000 * 2, 16000 * 2 + 77, 16000 * 3, 16000 + 5]
+    feats = [pyoracle.Fbank().compute(synth.pcm(90 + i, n)) for i, n in enumerate(lens)]
+    args = []
+    for i, f in enumerate(feats):
+        args += [_put(tmp_path, f"x{i}.f32", f), len(f)]
+    conf = _am_config(tmp_path, xs_config, 50, extra="gpu_batch_streams = 4\ngpu_batch_wait_us = 3000\n")
+    r = subprocess.run([DRIVER, "am_mt_fail", str(conf), str(tmp_path / "mt")] + [str(a) for a in args],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    calls, blocks, failed = [int(v) for v in r.stdout.split()[1::2]]
+    assert 1 <= failed <= len(feats)
+    assert calls >= 1
+    # the streams outside the failed batch completed with full output
+    done = [i for i in range(len(feats)) if (tmp_path / f"mt{i}.bin").exists()]
+    assert len(done) == len(feats) - failed
+    for i in done:
+        assert _load(tmp_path / f"mt{i}.bin").shape[0] == len(feats[i])
 
 
 @pytest.mark.gpu

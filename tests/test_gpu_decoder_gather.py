@@ -68,6 +68,13 @@ def test_loglik_gather_edges(torch, G, ctx, scored):
     trans = torch.tensor([1, 1, 1, -5, tpm.numel()], dtype=torch.int32, device="cuda")
     got = G.loglik_gather(ctx, ll, tpm, rows, trans).cpu().numpy()
     assert np.isfinite(got[0]) and np.isnan(got[1:]).all()
+    # a corrupt tid2pdf entry (pdf outside the row) also gives NaN, never a
+    # read past the row
+    bad = torch.tensor([0, ll.shape[1], -1, 2**30], dtype=torch.int32, device="cuda")
+    rows = torch.tensor([0, 0, 0, ll.shape[0] - 1], dtype=torch.int32, device="cuda")
+    trans = torch.tensor([0, 1, 2, 3], dtype=torch.int32, device="cuda")
+    got = G.loglik_gather(ctx, ll, bad, rows, trans).cpu().numpy()
+    assert np.isfinite(got[0]) and np.isnan(got[1:]).all()
 
 
 def test_loglik_columns(torch, G, ctx, scored):

@@ -62,6 +62,28 @@ def test_int8_block_bit_exact(torch, G, ctx, oracle, rows):
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
 
 
+def test_int8_blocks_are_independent(torch, G, ctx, oracle):
+    """ce_gpu_nnet_propagate_blocks on an int8 model: every block's rows equal
+    the block scored alone (per-block quantization parameters), and match the
+    oracle bit for bit -- the batcher's contract holds for int8 too."""
+    from catears_amd import formats
+    layers, left, right, _ = _tdnn(64, 96, final_logsm=False)
+    model = G.Model(ctx, image=formats.nnet_bytes(layers, left, right)).quantize(ctx)
+    rng = np.random.default_rng(77)
+    sizes = [70, 33, 151]
+    blocks = [rng.normal(9.0 + 4 * i, 1.0 + 2 * i, size=(n, 40)).astype(np.float32) for i, n in enumerate(sizes)]
+    got = G.nnet_propagate_blocks(ctx, model, dev(torch, np.concatenate(blocks)), sizes).cpu().numpy()
+    at = 0
+    for b in blocks:
+        alone = G.nnet_propagate(ctx, model, dev(torch, b)).cpu().numpy()
+        want = oracle.nnet_propagate_int8(layers, b)
+        part = got[at:at + len(alone)]
+        assert np.array_equal(part.view(np.uint32), alone.view(np.uint32))
+        assert np.array_equal(part.view(np.uint32), want.view(np.uint32))
+        at += len(alone)
+    assert at == len(got)
+
+
 def test_int8_am_forward_matches_oracle(torch, G, ctx, oracle, xs_config):
     from catears_amd import formats, synth
     am = formats.read_am(xs_config)

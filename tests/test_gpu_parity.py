@@ -168,6 +168,29 @@ def test_am_xs_vs_oracle(torch, G, ctx, oracle, xs_config, gemm):
             assert np.abs(o[off[u]:off[u + 1]] - ref).max() <= LOGLIK_TOL, f"utt {u}"
 
 
+def test_long_propagate_runs_in_exact_windows(torch, G, ctx, oracle, xs_config):
+    """ce_gpu_nnet_propagate on a block longer than its 65536-row window:
+    the windowed pass gives the same bits as scoring two overlapping halves
+    separately, and the rows around the window seam match the oracle."""
+    from catears_amd import formats
+    am = formats.read_am(xs_config)
+    model = G.Model(ctx, xs_config)
+    ctx_rows = model.left + model.right
+    rows = (1 << 16) + 3001
+    x = np.random.default_rng(65).normal(9.0, 3.0, size=(rows, 40)).astype(np.float32)
+    dx = dev(torch, x)
+    got = G.nnet_propagate(ctx, model, dx).cpu().numpy()
+    assert got.shape == (rows - ctx_rows, 512)
+    cut = 40000
+    a = G.nnet_propagate(ctx, model, dx[:cut + ctx_rows]).cpu().numpy()
+    b = G.nnet_propagate(ctx, model, dx[cut:]).cpu().numpy()
+    assert np.array_equal(bits(got), bits(np.concatenate([a, b])))
+    seam = (1 << 16) - ctx_rows
+    lo, hi = seam - 40, seam + 40
+    want = oracle.nnet_propagate(am["layers"], x[lo:hi + ctx_rows])
+    assert np.abs(got[lo:hi] - want).max() <= LOGLIK_TOL
+
+
 @pytest.mark.parametrize("gemm", ["fp32", "bf16x6", "bf16x6p", "f16x3"])
 def test_am_segmentation_is_exact(torch, G, ctx, oracle, xs_config, gemm):
     """Splitting an utterance over chunks (max_rows) must not change a bit:
