@@ -28,6 +28,14 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+# Hardware queues per process (HIP default 4): the pipeline's one front and
+# three nnet streams get one each.  Set before torch initialises HIP.
+# (measured: 8 queues with two front streams cost 5-6 % against the default
+# 4 with one; kept as an experiment knob, CATEARS_HW_QUEUES)
+HW_QUEUES = int(os.environ.get("CATEARS_HW_QUEUES", "4"))
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < HW_QUEUES:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
+
 FLOPS_PER_FRAME = 2 * (200 * 1024 + 4 * 3072 * 1024 + 1024 * 1024 + 1024 * 3456)  # 34,750,464
 # FLOPs per output frame of the GEMMs timed as CE_GPU_PROF_GEMM (all but layer 1)
 FLOPS_PER_FRAME_FAST = FLOPS_PER_FRAME - 2 * 200 * 1024
@@ -57,6 +65,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="minimum wall time of the CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the HIP-event kernel timing")
+    ap.add_argument("--stage-profile", action="store_true",
+                    help="time every kernel class (fbank, CMVN, splice, finalize) besides the GEMM; by default "
+                         "only the GEMM launches carry events (one per launch), which the roofline needs")
     ap.add_argument("--serial", action="store_true", help="one stream: no front/back stage overlap")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL) for real runs; gloo only to rehearse N ranks on one GPU "
@@ -68,6 +79,8 @@ def parse():
     ap.add_argument("--gemm", choices=["fp32", "bf16x6", "bf16x6p", "f16x3"], default=None,
                     help="matrix-core form of the fp32 Linear layers (ce_gpu_model_set_gemm); default: "
                          "the library's (bf16x6: three exact bf16 planes, six products, fp32 GEMM)")
+    ap.add_argument("--front-streams", type=int, default=1,
+                    help="fbank + CMVN streams; consecutive batches alternate between them")
     ap.add_argument("--back-streams", type=int, default=3,
                     help="nnet streams; consecutive batches alternate between them so one batch's "
                          "wave-quantisation tail overlaps the next batch's layers")
@@ -338,10 +351,14 @@ def main():
     # Every batch is still scored end to end inside the timed region.
     NB = 1 if args.serial else max(1, args.back_streams)
     backs = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(NB - 1)]
-    front = torch.cuda.Stream() if not args.serial else backs[0]
+    # --front-streams 2 alternates batches between two front streams (batch
+    # 1's fbank + CMVN beside batch 0's); measured slower than one (6 %: the
+    # second front stream's fbank blocks displace GEMM blocks from CUs)
+    NF = 1 if args.serial else max(1, args.front_streams)
+    fronts = [torch.cuda.Stream() for _ in range(NF)] if not args.serial else [backs[0]]
     ctxs = [gpu.Context(local, b) for b in backs]
     ctx = ctxs[0]
-    ctx_f = gpu.Context(local, front) if not args.serial else ctx
+    ctx_fs = [gpu.Context(local, f) for f in fronts] if not args.serial else [ctx]
     int8 = args.workload == "c5"
     model = gpu.Model(ctx, conf)
     if args.gemm:
@@ -360,7 +377,12 @@ def main():
     pool = max(args.pool, U)
     pcm = torch.from_numpy(np.stack([synth.pcm(rank * 100003 + i, n_samp) for i in range(pool)])).cuda()
     gstats = None if args.no_cmvn else torch.from_numpy(synth.cmvn_stats_synthetic()).cuda()
-    F = NB + 1  # feature slots: one being filled while NB are being scored
+    # feature slots: NB being scored plus NB + 2 already featurised, so the
+    # front stream runs a whole round of batches ahead and a stream that
+    # finishes a batch finds the next one's features ready (with NB + 1 slots
+    # the front waited for each batch's completion: a ~0.3 ms bubble per
+    # round of NB batches, tools/timeline.py)
+    F = 2 * NB + 2 if not args.serial else 2
     raw = [torch.empty((frames_per_step, 40), dtype=torch.float32, device="cuda") for _ in range(F)]
     norm = [torch.empty_like(raw[0]) for _ in range(F)] if gstats is not None else raw
     ready = [torch.cuda.Event() for _ in range(F)]
@@ -376,6 +398,7 @@ def main():
 
     def front_stage(i):
         slot = i % F
+        front, ctx_f = fronts[i % NF], ctx_fs[i % NF]
         front.wait_event(free[slot])  # the batch F steps ago has finished reading this slot
         first = (i * U) % (pool - U + 1)
         src = pcm[first:first + U].reshape(-1)
@@ -421,8 +444,8 @@ def main():
     torch.cuda.synchronize()
     if not args.no_profile:
         gpu.profile_anchor(local, backs[0])
-        for c in set(ctxs + [ctx_f]):
-            c.profile(True)
+        for c in set(ctxs + ctx_fs):
+            c.profile(True, classes=None if args.stage_profile or int8 else [ctx.PROF_GEMM])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -442,14 +465,14 @@ def main():
         checksum += gat.checksum
     finite = bool(torch.isfinite(outs[0]).all().item())
     # f16x3: no activation left the two-plane range in any batch
-    overflow = any(c.overflow() for c in set(ctxs + [ctx_f]))
+    overflow = any(c.overflow() for c in set(ctxs + ctx_fs))
 
     prof = {}
     if not args.no_profile:
-        for c in set(ctxs + [ctx_f]):
+        for c in set(ctxs + ctx_fs):
             c.profile(False)
         for name, cs, cls in (("gemm", ctxs, ctx.PROF_GEMM), ("gemm_gather", ctxs, ctx.PROF_GEMM_GATHER),
-                              ("fbank", [ctx_f], ctx.PROF_FBANK), ("cmvn", [ctx_f], ctx.PROF_CMVN),
+                              ("fbank", ctx_fs, ctx.PROF_FBANK), ("cmvn", ctx_fs, ctx.PROF_CMVN),
                               ("finalize", ctxs, ctx.PROF_FINALIZE), ("quantize", ctxs, ctx.PROF_QUANT)):
             iv = []
             for c in cs:

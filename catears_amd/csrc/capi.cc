@@ -599,19 +599,36 @@ static hipEvent_t pool_event(ce_gpu_ctx *ctx) {
 }
 
 ProfScope::ProfScope(ce_gpu_ctx *c, int k) : ctx(c), cls(k) {
-  if (!ctx->profiling) return;
-  hipEvent_t a = pool_event(ctx);
-  b = pool_event(ctx);
-  if (!a || !b) {
-    b = nullptr;
+  if (!ctx->profiling || !(ctx->prof_mask & (1u << cls))) {
+    ctx->chain_end = nullptr;  // an untimed launch breaks a chain
     return;
   }
-  (void)hipEventRecord(a, ctx->stream);
-  ctx->timed.push_back({cls, a, b});
+  hipEvent_t a = nullptr;
+  bool own_a = true;
+  if (ctx->chain_open && ctx->chain_end && ctx->chain_cls == cls) {
+    a = ctx->chain_end;
+    own_a = false;
+  } else {
+    a = pool_event(ctx);
+    if (!a) return;
+  }
+  b = pool_event(ctx);
+  if (!b) {
+    if (own_a) ctx->event_pool.push_back(a);
+    ctx->chain_end = nullptr;
+    return;
+  }
+  if (own_a) (void)hipEventRecord(a, ctx->stream);
+  ctx->timed.push_back({cls, a, b, own_a});
 }
 
 ProfScope::~ProfScope() {
-  if (b) (void)hipEventRecord(b, ctx->stream);
+  if (!b) return;
+  (void)hipEventRecord(b, ctx->stream);
+  if (ctx->chain_open) {
+    ctx->chain_end = b;
+    ctx->chain_cls = cls;
+  }
 }
 
 }  // namespace catears
@@ -647,7 +664,10 @@ int ce_gpu_ctx_destroy(ce_gpu_ctx *ctx) {
   if (!ctx) return CE_GPU_OK;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
-  for (auto &t : ctx->timed) (void)hipEventDestroy(t.a), (void)hipEventDestroy(t.b);
+  for (auto &t : ctx->timed) {
+    if (t.own_a) (void)hipEventDestroy(t.a);
+    (void)hipEventDestroy(t.b);
+  }
   for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
   delete ctx;
   return CE_GPU_OK;
@@ -694,6 +714,12 @@ int ce_gpu_ctx_profile(ce_gpu_ctx *ctx, int enable) {
   return CE_GPU_OK;
 }
 
+int ce_gpu_ctx_profile_classes(ce_gpu_ctx *ctx, unsigned mask) {
+  if (!ctx) return fail(CE_GPU_EINVAL, "ctx is NULL");
+  ctx->prof_mask = mask;
+  return CE_GPU_OK;
+}
+
 int ce_gpu_ctx_profile_read(ce_gpu_ctx *ctx, int kernel_class, double *total_ms, int64_t *launches) {
   if (!ctx || kernel_class < 0 || kernel_class >= CE_GPU_PROF_CLASSES) return fail(CE_GPU_EINVAL, "bad argument");
   CE_HIP(hipStreamSynchronize(ctx->stream));
@@ -709,7 +735,7 @@ int ce_gpu_ctx_profile_read(ce_gpu_ctx *ctx, int kernel_class, double *total_ms,
     CE_HIP(hipEventElapsedTime(&e, t.a, t.b));
     ms += e;
     ++n;
-    ctx->event_pool.push_back(t.a);
+    if (t.own_a) ctx->event_pool.push_back(t.a);
     ctx->event_pool.push_back(t.b);
   }
   ctx->timed.swap(keep);
@@ -754,7 +780,7 @@ int ce_gpu_ctx_profile_intervals(ce_gpu_ctx *ctx, int kernel_class, double *h_st
     h_start_ms[i] = a;
     h_end_ms[i] = b;
     ++i;
-    ctx->event_pool.push_back(t.a);
+    if (t.own_a) ctx->event_pool.push_back(t.a);
     ctx->event_pool.push_back(t.b);
   }
   ctx->timed.swap(keep);
@@ -1068,6 +1094,7 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
   float *out = ctx->workspace.as<float>() + 2 * blk;
   const float *xs = nullptr;
   int px = 0, cur = 0;
+  ProfChain chain(ctx);  // every step below is one launch; GEMMs back to back
   for (size_t i = 0; i < m->steps.size(); ++i) {
     const GemmLayer &g = m->steps[i].gemm;
     const bool last = i + 1 == m->steps.size();
@@ -1089,6 +1116,8 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
     a.ldx = px;
     a.wf = g.wt.as<float>();
     a.ldw = g.kpad;
+    a.w = g.wsplit.as<uint16_t>();  // the same weights as planes (kernels that read them)
+    a.pw = g.kpad;
     a.m = rows;
     a.n = g.n;
     a.kpad = i == 0 ? g.kpad : g.nseg * g.din;

@@ -227,22 +227,44 @@ struct ce_gpu_ctx {
   std::vector<int32_t> h_blk_maps;
   // optional per-class launch timing (ce_gpu_ctx_profile)
   bool profiling = false;
+  unsigned prof_mask = ~0u;  // classes timed while profiling (ce_gpu_ctx_profile_classes)
   struct Timed {
     int cls;
     hipEvent_t a, b;
+    bool own_a;  // false: a is the previous launch's b (chained, see ProfChain)
   };
+  // consecutive launches of one class inside a ProfChain share the boundary
+  // event: the previous launch's end is this launch's start
+  bool chain_open = false;
+  int chain_cls = -1;
+  hipEvent_t chain_end = nullptr;
   std::vector<Timed> timed;
   std::vector<hipEvent_t> event_pool;
 };
 
 namespace catears {
-// Brackets one launch with events when ctx->profiling is set.
+// Brackets one launch with events when ctx->profiling is set (and the
+// class is in ctx->prof_mask).
 struct ProfScope {
   ce_gpu_ctx *ctx;
   int cls;
   hipEvent_t b = nullptr;
   ProfScope(ce_gpu_ctx *c, int k);
   ~ProfScope();
+};
+// Within its scope, back-to-back launches of one class on the context's
+// stream (nothing else enqueued between them) are timed with one event per
+// launch instead of two: fewer event records in the timed region.
+struct ProfChain {
+  ce_gpu_ctx *ctx;
+  explicit ProfChain(ce_gpu_ctx *c) : ctx(c) {
+    ctx->chain_open = true;
+    ctx->chain_end = nullptr;
+  }
+  ~ProfChain() {
+    ctx->chain_open = false;
+    ctx->chain_end = nullptr;
+  }
 };
 }  // namespace catears
 

@@ -20,12 +20,33 @@ namespace {
 constexpr int kWindow = 600;  // PK_ONLINECMVN_WINDOW, src/cmvn.h:10
 constexpr int kGlobal = 200;  // PK_ONLINECMVN_GLOBALFRAMES, src/cmvn.h:11
 
-constexpr int kTile = 32;  // frames prefetched into registers per step of the chain
+constexpr int kTile = 24;  // frames prefetched into registers per tile of the chain
+
+// The chain of one (utterance, dimension) runs in three regimes of t:
+//   t <  599: SmoothStats adds alpha_t * [g, N_g] (count = t + 1 < 600);
+//   t == 599: count = 600, neither smoothing nor window subtraction;
+//   t >= 600: frame t - 600 leaves the window (no smoothing).
+// Each regime is its own loop, so no step carries a select, and the per-step
+// work is the reference's arithmetic only (the kernel is issue-bound: one
+// wave per utterance, a latency chain per lane).
+enum CmvnMode { kSmooth, kPlain, kWindowed };
+
+template <int M>
+__device__ __forceinline__ float cmvn_step(float &carry, float c, float o, float al, float ng, float g) {
+  // ComputeStats (cmvn.cc:35-68): double temp seeded from the float carry
+  double acc = (double)carry;
+  acc += (double)c;
+  if (M == kWindowed) acc += -1.0 * (double)o;
+  carry = (float)acc;
+  float s = carry;
+  if (M == kSmooth) s = al != 1.0f ? s + al * g : s + g;  // SmoothStats (cmvn.cc:80-88)
+  return ng != 1.0f ? c + ng * s : c + s;                 // Apply (cmvn.cc:91-98)
+}
 
 // Everything in SmoothStats/Apply except the per-dimension sums depends only
 // on the frame index t (count = min(t+1, 600)) and on N_g, so it is computed
 // once per block into LDS: alpha_t (the float scalar of AddVec, cmvn.cc:80-88)
-// and neg_t = -(float)(1 / smoothed count) (cmvn.cc:93-97).  For t >= 600 no
+// and neg_t = -(float)(1 / smoothed count) (cmvn.cc:93-97).  For t >= 599 no
 // smoothing happens and the count is exactly 600.
 __global__ __launch_bounds__(64) void cmvn_kernel(const int64_t *__restrict__ frame_off,
                                                   const float *__restrict__ gstats,
@@ -49,56 +70,69 @@ __global__ __launch_bounds__(64) void cmvn_kernel(const int64_t *__restrict__ fr
   __syncthreads();
   if (d >= kMel) return;
   const int64_t r0 = frame_off[u];
-  const int t_frames = (int)(frame_off[u + 1] - r0);
+  const int T = (int)(frame_off[u + 1] - r0);
+  if (T == 0) return;
   const float g = gstats[d];
   const float *x = in + r0 * kMel + d;
   float *y = out + r0 * kMel + d;
-  float cur[kTile], old[kTile], ncur[kTile], nold[kTile];
-  // Unconditional loads at clamped (always valid) frames: a per-element
-  // "load or zero" select makes hipcc branch around every load and wait
-  // vmcnt(0) each time.  Frames past the end are never used.
-  if (t_frames == 0) return;
-  auto fetch = [&](int t0, float *c, float *o) {
-#pragma unroll
-    for (int i = 0; i < kTile; ++i) {
-      const int t = min(t0 + i, t_frames - 1);
-      c[i] = x[(int64_t)t * kMel];
-      o[i] = x[(int64_t)max(t - kWindow, 0) * kMel];
-    }
-  };
-  // per-frame scalars of a tile, read from LDS before the chain runs (a read
-  // per step would put an LDS round trip on the critical path)
-  float al[kTile], ng[kTile];
-  auto scalars = [&](int t0) {
-#pragma unroll
-    for (int i = 0; i < kTile; ++i) {
-      const int t = t0 + i;
-      al[i] = s_alpha[min(t, kWindow - 1)];
-      ng[i] = s_neg[min(t, kWindow)];
-    }
-  };
-  fetch(0, cur, old);
+  const float ng600 = s_neg[kWindow];
   float carry = 0.0f;
-  for (int t0 = 0; t0 < t_frames; t0 += kTile) {
-    fetch(t0 + kTile, ncur, nold);
-    scalars(t0);
+
+  // Frames [t0, t1) in regime M.  Whole tiles: the next tile's rows are
+  // prefetched from a base clamped into [0, t1 - kTile] (all valid rows, one
+  // base + immediate offsets per tile); the last, partial tile reloads with
+  // per-row clamps.
+  auto phase = [&](auto MC, int t0, int t1) {
+    constexpr int M = decltype(MC)::value;
+    if (t0 >= t1) return;
+    float c[kTile], o[kTile];
+    auto load_tile = [&](int b, float *cc, float *oo) {
+      const float *xc = x + (int64_t)b * kMel;
 #pragma unroll
-    for (int i = 0; i < kTile; ++i) {
-      const int t = t0 + i;
-      if (t < t_frames) {
-        // ComputeStats (cmvn.cc:35-68): double temp seeded from the float carry
-        double acc = t > 0 ? (double)carry : 0.0;
-        acc += (double)cur[i];
-        if (t >= kWindow) acc += -1.0 * (double)old[i];
-        carry = (float)acc;
-        float s = carry;
-        if (t < kWindow) s = al[i] != 1.0f ? s + al[i] * g : s + g;
-        y[(int64_t)t * kMel] = ng[i] != 1.0f ? cur[i] + ng[i] * s : cur[i] + s;
+      for (int i = 0; i < kTile; ++i) cc[i] = xc[i * kMel];
+      if (M == kWindowed) {
+        const float *xo = x + (int64_t)max(b - kWindow, 0) * kMel;
+#pragma unroll
+        for (int i = 0; i < kTile; ++i) oo[i] = xo[i * kMel];
+      }
+    };
+    int t = t0;
+    if (t + kTile <= t1) load_tile(t, c, o);
+    for (; t + kTile <= t1; t += kTile) {
+      float cn[kTile], on[kTile];
+      load_tile(max(0, min(t + kTile, t1 - kTile)), cn, on);
+      float al[kTile], ng[kTile];
+#pragma unroll
+      for (int i = 0; i < kTile; ++i) {
+        al[i] = M == kSmooth ? s_alpha[t + i] : 0.0f;
+        ng[i] = M == kSmooth ? s_neg[t + i] : ng600;
+      }
+      float *yt = y + (int64_t)t * kMel;
+#pragma unroll
+      for (int i = 0; i < kTile; ++i) yt[i * kMel] = cmvn_step<M>(carry, c[i], o[i], al[i], ng[i], g);
+#pragma unroll
+      for (int i = 0; i < kTile; ++i) c[i] = cn[i], o[i] = on[i];
+    }
+    if (t < t1) {  // partial tile
+#pragma unroll
+      for (int i = 0; i < kTile; ++i) {
+        const int tt = min(t + i, t1 - 1);
+        c[i] = x[(int64_t)tt * kMel];
+        o[i] = M == kWindowed ? x[(int64_t)(tt - kWindow) * kMel] : 0.0f;
+      }
+#pragma unroll
+      for (int i = 0; i < kTile; ++i) {
+        if (t + i < t1) {
+          const float al = M == kSmooth ? s_alpha[t + i] : 0.0f;
+          const float ng = M == kSmooth ? s_neg[t + i] : ng600;
+          y[(int64_t)(t + i) * kMel] = cmvn_step<M>(carry, c[i], o[i], al, ng, g);
+        }
       }
     }
-#pragma unroll
-    for (int i = 0; i < kTile; ++i) cur[i] = ncur[i], old[i] = nold[i];
-  }
+  };
+  phase(std::integral_constant<int, kSmooth>(), 0, min(T, kWindow - 1));
+  phase(std::integral_constant<int, kPlain>(), kWindow - 1, min(T, kWindow));
+  phase(std::integral_constant<int, kWindowed>(), kWindow, T);
 }
 
 }  // namespace

@@ -20,7 +20,7 @@ ERRORS = {-2: "EINVAL", -3: "EHIP", -4: "EIO", -5: "ECORRUPT", -6: "ENOTSUP", -7
 # Every symbol include/catears_gpu.h declares (checked by tests).
 ABI = [
     "ce_gpu_last_error", "ce_gpu_version", "ce_gpu_ctx_create", "ce_gpu_ctx_destroy",
-    "ce_gpu_ctx_set_stream", "ce_gpu_ctx_synchronize", "ce_gpu_ctx_profile",
+    "ce_gpu_ctx_set_stream", "ce_gpu_ctx_synchronize", "ce_gpu_ctx_profile", "ce_gpu_ctx_profile_classes",
     "ce_gpu_ctx_profile_read", "ce_gpu_model_load_config",
     "ce_gpu_model_load", "ce_gpu_model_info", "ce_gpu_model_tid2pdf", "ce_gpu_model_destroy",
     "ce_gpu_fbank_num_frames", "ce_gpu_plan_create", "ce_gpu_plan_info",
@@ -64,6 +64,7 @@ def lib():
         "ce_gpu_ctx_set_stream": (ci, [vp, vp]),
         "ce_gpu_ctx_synchronize": (ci, [vp]),
         "ce_gpu_ctx_profile": (ci, [vp, ci]),
+        "ce_gpu_ctx_profile_classes": (ci, [vp, ctypes.c_uint]),
         "ce_gpu_ctx_profile_read": (ci, [vp, ci, ctypes.POINTER(ctypes.c_double), pi64]),
         "ce_gpu_model_load_config": (ci, [vp, ctypes.c_char_p, pp]),
         "ce_gpu_model_load": (ci, [vp, ctypes.c_char_p, ctypes.c_char_p, ci, ci, pp]),
@@ -149,7 +150,11 @@ class Context:
 
     PROF_GEMM, PROF_GEMM_GATHER, PROF_FBANK, PROF_CMVN, PROF_FINALIZE, PROF_QUANT = range(6)
 
-    def profile(self, enable=True):
+    def profile(self, enable=True, classes=None):
+        """Time launches (HIP events); `classes`: iterable of PROF_* to time
+        (default all)."""
+        mask = 0xffffffff if classes is None else sum(1 << c for c in classes)
+        check(lib().ce_gpu_ctx_profile_classes(self.h, mask))
         check(lib().ce_gpu_ctx_profile(self.h, int(enable)))
 
     def profile_read(self, cls):

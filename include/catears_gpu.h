@@ -95,6 +95,11 @@ int ce_gpu_ctx_overflow(ce_gpu_ctx *ctx, int *overflow);
 #define CE_GPU_PROF_QUANT 5 /* int8 path: per-layer min/max + quantize passes */
 #define CE_GPU_PROF_CLASSES 6
 int ce_gpu_ctx_profile(ce_gpu_ctx *ctx, int enable);
+/* Restrict the timing to the classes whose bit (1 << class) is set in
+ * `mask` (default: all).  Back-to-back GEMM launches of one call share their
+ * boundary events, so timing only CE_GPU_PROF_GEMM costs one event record
+ * per GEMM launch. */
+int ce_gpu_ctx_profile_classes(ce_gpu_ctx *ctx, unsigned mask);
 int ce_gpu_ctx_profile_read(ce_gpu_ctx *ctx, int kernel_class, double *total_ms, int64_t *launches);
 
 /* Per-launch intervals for kernels that overlap across streams: record a
