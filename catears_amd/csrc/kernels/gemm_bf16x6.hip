@@ -809,6 +809,77 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
   load(1);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
+  if constexpr (SCHED >= 4) {
+    // Staggered roles: each SIMD holds one wave of each half of the block
+    // (waves w and w + NW/2).  After the K-tile barrier the first half
+    // splits tile kt+1 into LDS (VALU + ds_write) and then runs the MFMAs of
+    // tile kt; the second half runs its MFMAs first and splits afterwards.
+    // So on every SIMD one wave's split VALU issues in the gaps of its
+    // partner's MFMAs, instead of both waves splitting at once with the
+    // matrix pipe idle (the SCHED 0 loop: one phase for all waves).  Same
+    // barrier count and LDS protocol:
+    //   WAR: stage (kt+1) % 2 was last read in tile kt-1, before the
+    //        barrier that closed it;
+    //   RAW: every wave's writes of stage kt+1 precede the barrier that
+    //        closes tile kt.
+    auto mfma_tile = [&](int kt) {
+      const char *st = smem + (kt & 1) * STAGE;
+      bf16x8 a[3][TW], b[3][TF];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+        for (int i = 0; i < TW; ++i)
+          a[pl][i] = *reinterpret_cast<const bf16x8 *>(st + (pl * BW + wrow + i * 16) * 64 + foff);
+#pragma unroll
+        for (int j = 0; j < TF; ++j)
+          b[pl][j] = *reinterpret_cast<const bf16x8 *>(st + 3 * BW * 64 + (pl * BF + frow + j * 16) * 64 + foff);
+      }
+#pragma unroll
+      for (int i = 0; i < TW; ++i)
+#pragma unroll
+        for (int j = 0; j < TF; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TW; ++i)
+#pragma unroll
+        for (int j = 0; j < TF; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[0][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[1][j], acc[i][j], 0, 0, 0);
+        }
+#pragma unroll
+      for (int i = 0; i < TW; ++i)
+#pragma unroll
+        for (int j = 0; j < TF; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[2][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2][i], b[0][j], acc[i][j], 0, 0, 0);
+        }
+    };
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    // SCHED 6: every wave in the second half's order (MFMAs of tile kt,
+    // then the split of tile kt+1, which the compiler interleaves into the
+    // MFMA stream)
+    if (SCHED == 6 || wv >= C::NW / 2) {
+      if constexpr (SCHED == 5) __builtin_amdgcn_s_setprio(1);
+      for (int kt = 0; kt < ktiles; ++kt) {
+        mfma_tile(kt);
+        store(kt + 1);
+        load(kt + 2);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      }
+    } else {
+      for (int kt = 0; kt < ktiles; ++kt) {
+        store(kt + 1);
+        load(kt + 2);
+        mfma_tile(kt);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    x6_epilogue<TW, TF, false>(p, acc, n0 + wrow, f0 + frow, lane);
+    return;
+  }
   for (int kt = 0; kt < ktiles; ++kt) {
     store(kt + 1);
     load(kt + 2);
@@ -1636,6 +1707,21 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
         return launch_f<X6Cfg<128, 256, 2, 2, 2>>(s, p);
       case 47:
         return launch_f<X6Cfg<256, 128, 4, 2, 2>, 2>(s, p);
+      // staggered split / MFMA roles per SIMD (SCHED 4; 5: + static priority for the second half)
+      case 51:
+        return launch_f<X6Cfg<128, 256, 2, 4, 2>, 4>(s, p);
+      case 52:
+        return launch_f<X6Cfg<128, 256, 2, 4, 2>, 5>(s, p);
+      case 53:
+        return launch_f<X6Cfg<128, 128, 2, 4, 2>, 4>(s, p);
+      case 54:
+        return launch_f<X6Cfg<256, 128, 4, 2, 2>, 4>(s, p);
+      case 55:
+        return launch_f<X6Cfg<128, 256, 2, 4, 2>, 6>(s, p);
+      case 56:
+        return launch_f<X6Cfg<128, 128, 2, 4, 2>, 6>(s, p);
+      case 57:
+        return launch_f<X6Cfg<256, 128, 4, 2, 2>, 6>(s, p);
       // 32x32x16 MFMA kernels; odd = weights from the load-time planes
       case 60:
         return launch_m<X6MCfg<128, 256, 2, 4>, false>(s, p);
@@ -1673,8 +1759,10 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
         return launch_c<X6CCfg<128, 256, 2, 4, 32>, false, 2>(s, p);
       case 83:
         return launch_c<X6CCfg<128, 256, 2, 4, 32>, false, 3>(s, p);
-      default:  // = 42
+      case 42:  // round-1 default: split of tile kt+1, then the MFMAs of tile kt
         return launch_f<X6Cfg<128, 256, 2, 4, 2>>(s, p);
+      default:  // = 55
+        return launch_f<X6Cfg<128, 256, 2, 4, 2>, 6>(s, p);
     }
   }
   switch (x6_variant()) {
