@@ -735,7 +735,12 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6z_kernel(X6Args p) {
 //        drained before step kt's barrier; step kt+1 reads after it.
 // Tiles past the end are clamped to the last one (written to a stage no
 // later step reads), so the body is one basic block.
-template <class C, int SCHED>
+// DIAG (ablation builds of the SCHED >= 4 loop, wrong results; timing only,
+// DESIGN.md §8): bit 1 = no split (raw fp32 bits as the three planes),
+// 2 = no global loads after the prologue, 4 = no MFMAs, 8 = no fragment
+// reads after the first tile, 16 = no K-tile barrier, 32 = no plane writes
+// after the prologue.
+template <class C, int SCHED, int DIAG = 0>
 __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
   constexpr int BW = C::BW, BF = C::BF, TW = C::TW, TF = C::TF, NT = C::NT, STAGE = C::STAGE;
   constexpr int RPP = NT / 4;  // rows per pass (4 threads x 32 B per row)
@@ -760,6 +765,9 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
   const int ktiles = p.kpad / 32;
   f32x4v rw0[NPW], rw1[NPW], rx0[NPX], rx1[NPX];
   auto load = [&](int kt) {
+    if constexpr ((DIAG & 2) != 0) {
+      if (kt > 1) return;
+    }
     kt = min(kt, ktiles - 1);
     const int k0 = kt * 32;
     const int seg = k0 / p.din, col0 = k0 - seg * p.din;
@@ -781,14 +789,23 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
   };
   // 8 floats -> three 16-B plane chunks at row r of the plane block `base`
   auto put = [&](char *base, int nrows, int r, f32x4v v0, f32x4v v1) {
-    const Planes2 q0 = split3_pair(v0.x, v0.y), q1 = split3_pair(v0.z, v0.w);
-    const Planes2 q2 = split3_pair(v1.x, v1.y), q3 = split3_pair(v1.z, v1.w);
+    Planes2 q0, q1, q2, q3;
+    if constexpr ((DIAG & 1) != 0) {
+      auto raw = [](float a) { const uint32_t u = __builtin_bit_cast(uint32_t, a); return Planes2{u, u, u}; };
+      q0 = raw(v0.x), q1 = raw(v0.z), q2 = raw(v1.x), q3 = raw(v1.z);
+    } else {
+      q0 = split3_pair(v0.x, v0.y), q1 = split3_pair(v0.z, v0.w);
+      q2 = split3_pair(v1.x, v1.y), q3 = split3_pair(v1.z, v1.w);
+    }
     const int off = r * 64 + ((pch ^ swz(r)) * 16);
     *reinterpret_cast<u32x4 *>(base + off) = u32x4{q0.h, q1.h, q2.h, q3.h};
     *reinterpret_cast<u32x4 *>(base + nrows * 64 + off) = u32x4{q0.m, q1.m, q2.m, q3.m};
     *reinterpret_cast<u32x4 *>(base + 2 * nrows * 64 + off) = u32x4{q0.l, q1.l, q2.l, q3.l};
   };
   auto store = [&](int kt) {
+    if constexpr ((DIAG & 32) != 0) {
+      if (kt > 1) return;
+    }
     char *st = smem + (kt & 1) * STAGE;
 #pragma unroll
     for (int i = 0; i < NPW; ++i) put(st, BW, prow + i * RPP, rw0[i], rw1[i]);
@@ -822,17 +839,29 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
     //        barrier that closed it;
     //   RAW: every wave's writes of stage kt+1 precede the barrier that
     //        closes tile kt.
+    bf16x8 a[3][TW], b[3][TF];
     auto mfma_tile = [&](int kt) {
       const char *st = smem + (kt & 1) * STAGE;
-      bf16x8 a[3][TW], b[3][TF];
+      if ((DIAG & 8) == 0 || kt == 0) {
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) {
+        for (int pl = 0; pl < 3; ++pl) {
 #pragma unroll
-        for (int i = 0; i < TW; ++i)
-          a[pl][i] = *reinterpret_cast<const bf16x8 *>(st + (pl * BW + wrow + i * 16) * 64 + foff);
+          for (int i = 0; i < TW; ++i)
+            a[pl][i] = *reinterpret_cast<const bf16x8 *>(st + (pl * BW + wrow + i * 16) * 64 + foff);
 #pragma unroll
-        for (int j = 0; j < TF; ++j)
-          b[pl][j] = *reinterpret_cast<const bf16x8 *>(st + 3 * BW * 64 + (pl * BF + frow + j * 16) * 64 + foff);
+          for (int j = 0; j < TF; ++j)
+            b[pl][j] = *reinterpret_cast<const bf16x8 *>(st + 3 * BW * 64 + (pl * BF + frow + j * 16) * 64 + foff);
+        }
+      }
+      if constexpr ((DIAG & 4) != 0) {
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+          for (int i = 0; i < TW; ++i) asm volatile("" ::"v"(a[pl][i]));
+#pragma unroll
+          for (int j = 0; j < TF; ++j) asm volatile("" ::"v"(b[pl][j]));
+        }
+        return;
       }
 #pragma unroll
       for (int i = 0; i < TW; ++i)
@@ -854,18 +883,122 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2][i], b[0][j], acc[i][j], 0, 0, 0);
         }
     };
+    if constexpr (SCHED == 8) {
+      // Region-scheduled loop (sched_barrier between regions; the compiler
+      // interleaves inside each): plane 0 and 1 fragment reads + the 16
+      // plane-0 MFMAs + the weight-row split of tile kt+1 and the weight
+      // loads of tile kt+2 | half the plane-1 MFMAs + activation row 0's
+      // split and loads | the other half + row 1 + plane-2 reads | the 32
+      // plane-2 MFMAs.  Each load is issued as soon as the split has freed
+      // its registers, about one iteration before its data is split.
+      static_assert(NPW == 1 && NPX == 2 && TW % 2 == 0, "SCHED 8 geometry");
+      auto read_plane = [&](const char *st, int pl) {
+#pragma unroll
+        for (int i = 0; i < TW; ++i)
+          a[pl][i] = *reinterpret_cast<const bf16x8 *>(st + (pl * BW + wrow + i * 16) * 64 + foff);
+#pragma unroll
+        for (int j = 0; j < TF; ++j)
+          b[pl][j] = *reinterpret_cast<const bf16x8 *>(st + 3 * BW * 64 + (pl * BF + frow + j * 16) * 64 + foff);
+      };
+      auto kpos = [&](int kt, int *k0, int *col0, int *shift) {
+        kt = min(kt, ktiles - 1);
+        *k0 = kt * 32;
+        const int seg = *k0 / p.din;
+        *col0 = *k0 - seg * p.din;
+        *shift = (int)(signed char)(p.off_packed >> (8 * seg));
+      };
+      auto load_w = [&](int kt) {
+        int k0, col0, shift;
+        kpos(kt, &k0, &col0, &shift);
+        gvec *wb = (gvec *)(p.wf + k0);
+        rw0[0] = wb[wsrc[0] / 4];
+        rw1[0] = wb[wsrc[0] / 4 + 1];
+      };
+      auto load_x = [&](int kt, int i) {
+        int k0, col0, shift;
+        kpos(kt, &k0, &col0, &shift);
+        gvec *xb = (gvec *)(p.xf + col0 + 8 * pch);
+        const int src = clampi(f0 + prow + i * RPP + shift, 0, p.m - 1);
+        const uint32_t o = (uint32_t)(src * p.ldx) / 4;
+        rx0[i] = xb[o];
+        rx1[i] = xb[o + 1];
+      };
+      for (int kt = 0; kt < ktiles; ++kt) {
+        const char *st = smem + (kt & 1) * STAGE;
+        char *sn = smem + ((kt + 1) & 1) * STAGE;
+        read_plane(st, 0);
+        read_plane(st, 1);
+#pragma unroll
+        for (int i = 0; i < TW; ++i)
+#pragma unroll
+          for (int j = 0; j < TF; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
+        put(sn, BW, prow, rw0[0], rw1[0]);
+        load_w(kt + 2);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+          for (int i = h * TW / 2; i < (h + 1) * TW / 2; ++i)
+#pragma unroll
+            for (int j = 0; j < TF; ++j) {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[1][j], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[0][j], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[1][j], acc[i][j], 0, 0, 0);
+            }
+          put(sn + 3 * BW * 64, BF, prow + h * RPP, rx0[h], rx1[h]);
+          load_x(kt + 2, h);
+          if (h == 1) read_plane(st, 2);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int i = 0; i < TW; ++i)
+#pragma unroll
+          for (int j = 0; j < TF; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[2][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2][i], b[0][j], acc[i][j], 0, 0, 0);
+          }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      x6_epilogue<TW, TF, false>(p, acc, n0 + wrow, f0 + frow, lane);
+      return;
+    }
     const int wv = __builtin_amdgcn_readfirstlane(wave);
     // SCHED 6: every wave in the second half's order (MFMAs of tile kt,
     // then the split of tile kt+1, which the compiler interleaves into the
     // MFMA stream)
-    if (SCHED == 6 || wv >= C::NW / 2) {
+    if (SCHED >= 6 || wv >= C::NW / 2) {
       if constexpr (SCHED == 5) __builtin_amdgcn_s_setprio(1);
       for (int kt = 0; kt < ktiles; ++kt) {
         mfma_tile(kt);
         store(kt + 1);
         load(kt + 2);
+        if constexpr (SCHED == 7) {
+          // explicit interleave: the split of tile kt+1 in the first third
+          // of the MFMA stream, then the loads of tile kt+2 (so they have
+          // two thirds of this iteration and the next barrier to land), then
+          // the plane writes; fragment reads of planes 1 / 2 spread early
+          constexpr int NMM = 6 * TW * TF, NRD = 3 * (TW + TF), NR0 = TW + TF;
+          constexpr int NV = 5, NSPL = NMM / 3;
+          __builtin_amdgcn_sched_group_barrier(0x100, NR0, 0);
+#pragma unroll
+          for (int g = 0; g < NSPL; ++g) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
+            if (g % 2 == 0 && g / 2 < NRD - NR0) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x020, 2 * (NPW + NPX), 0);
+#pragma unroll
+          for (int g = 0; g < 3 * (NPW + NPX); ++g) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, NMM - NSPL - 3 * (NPW + NPX), 0);
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
+        if constexpr ((DIAG & 16) == 0) __builtin_amdgcn_s_barrier();
       }
     } else {
       for (int kt = 0; kt < ktiles; ++kt) {
@@ -947,6 +1080,347 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   x6_epilogue<TW, TF, false>(p, acc, n0 + wrow, f0 + frow, lane);
+}
+
+// Weights in LDS, activations in registers (gemm_bf16x6w_kernel).  The
+// block's 8 waves all span the tile's BW units and split its BF frames (BF/8
+// per wave), so each activation element feeds exactly one wave: the wave
+// loads its own rows straight into registers in the MFMA B-operand layout
+// (lane l: frame l % 16, k = 8 (l / 16) .. +8 -- 32 contiguous bytes of one
+// row, one 128-B line per row over 4 lanes) and splits them into the three
+// bf16 planes in registers.  Only the weight planes go through LDS (written
+// once per block, read by all 8 waves), so the LDS write traffic per K-tile
+// drops from (BW + BF) to BW rows x 192 B: the plane writes were the largest
+// single overhead of the fp32-operand kernel (ablation: -21 % time without
+// them).  Same split, same products, same accumulation order
+// per output as gemm_bf16x6f_kernel: bit-identical results.
+template <int BW_, int BF_, int NW_>
+struct X6WCfg {
+  static constexpr int BW = BW_, BF = BF_, NW = NW_, NT = 64 * NW;
+  static constexpr int TW = BW / 16, TF = BF / NW / 16;  // 16 x 16 fragments per wave
+  static constexpr int STAGE = 3 * BW * 64;               // weight planes per K-tile (bytes)
+  static constexpr int RPP = NT / 4;                      // weight rows per pass
+  static constexpr int NPW = BW / RPP < 1 ? 1 : BW / RPP;
+  static_assert(TF >= 1 && BF % (NW * 16) == 0, "bad X6W tile");
+};
+
+template <class C, int SCHED>
+__global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6w_kernel(X6Args p) {
+  constexpr int BW = C::BW, TW = C::TW, TF = C::TF, NPW = C::NPW, RPP = C::RPP, STAGE = C::STAGE;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  auto swz = [](int row) { return ((row >> 3) & 1) << 1; };
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef const __attribute__((address_space(1))) f32x4v gvec;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int tm, tn;
+  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
+  const int f0 = tm * C::BF, n0 = tn * BW;
+  const int prow = tid >> 2, pch = tid & 3;
+  const bool wload = BW >= RPP || prow < BW;  // threads that stage weight rows
+  const int ktiles = p.kpad / 32;
+
+  uint32_t wsrc[NPW];  // float offset of this thread's weight row at k = 0
+#pragma unroll
+  for (int i = 0; i < NPW; ++i) wsrc[i] = (uint32_t)(min(n0 + min(prow + i * RPP, BW - 1), p.n - 1) * p.ldw + 8 * pch);
+  const int fw = f0 + wave * (TF * 16);  // this wave's first frame
+  const int kq = (lane >> 4) * 8;
+  f32x4v rw0[NPW], rw1[NPW], rx0[TF], rx1[TF];
+
+  auto load_w = [&](int kt) {
+    kt = min(kt, ktiles - 1);
+    gvec *wb = (gvec *)(p.wf + kt * 32);
+#pragma unroll
+    for (int i = 0; i < NPW; ++i) {
+      rw0[i] = wb[wsrc[i] / 4];
+      rw1[i] = wb[wsrc[i] / 4 + 1];
+    }
+  };
+  auto load_x = [&](int kt) {
+    kt = min(kt, ktiles - 1);
+    const int k0 = kt * 32;
+    const int seg = k0 / p.din, col0 = k0 - seg * p.din;
+    const int shift = (int)(signed char)(p.off_packed >> (8 * seg));
+    gvec *xb = (gvec *)(p.xf + col0 + kq);
+#pragma unroll
+    for (int j = 0; j < TF; ++j) {
+      const int src = clampi(fw + j * 16 + (lane & 15) + shift, 0, p.m - 1);
+      const uint32_t o = (uint32_t)(src * p.ldx) / 4;
+      rx0[j] = xb[o];
+      rx1[j] = xb[o + 1];
+    }
+  };
+  auto put_w = [&](int kt) {
+    if (!wload) return;
+    char *st = smem + (kt & 1) * STAGE;
+#pragma unroll
+    for (int i = 0; i < NPW; ++i) {
+      const int r = prow + i * RPP;
+      const Planes2 q0 = split3_pair(rw0[i].x, rw0[i].y), q1 = split3_pair(rw0[i].z, rw0[i].w);
+      const Planes2 q2 = split3_pair(rw1[i].x, rw1[i].y), q3 = split3_pair(rw1[i].z, rw1[i].w);
+      const int off = r * 64 + ((pch ^ swz(r)) * 16);
+      *reinterpret_cast<u32x4 *>(st + off) = u32x4{q0.h, q1.h, q2.h, q3.h};
+      *reinterpret_cast<u32x4 *>(st + BW * 64 + off) = u32x4{q0.m, q1.m, q2.m, q3.m};
+      *reinterpret_cast<u32x4 *>(st + 2 * BW * 64 + off) = u32x4{q0.l, q1.l, q2.l, q3.l};
+    }
+  };
+  auto split_x = [&](bf16x8 (&b)[3][TF]) {
+#pragma unroll
+    for (int j = 0; j < TF; ++j) {
+      const Planes2 q0 = split3_pair(rx0[j].x, rx0[j].y), q1 = split3_pair(rx0[j].z, rx0[j].w);
+      const Planes2 q2 = split3_pair(rx1[j].x, rx1[j].y), q3 = split3_pair(rx1[j].z, rx1[j].w);
+      b[0][j] = __builtin_bit_cast(bf16x8, (u32x4{q0.h, q1.h, q2.h, q3.h}));
+      b[1][j] = __builtin_bit_cast(bf16x8, (u32x4{q0.m, q1.m, q2.m, q3.m}));
+      b[2][j] = __builtin_bit_cast(bf16x8, (u32x4{q0.l, q1.l, q2.l, q3.l}));
+    }
+  };
+
+  const int foff = (lane & 15) * 64 + (((lane >> 4) ^ (((lane >> 3) & 1) << 1)) * 16);
+  f32x4 acc[TW][TF];
+#pragma unroll
+  for (int i = 0; i < TW; ++i)
+#pragma unroll
+    for (int j = 0; j < TF; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+
+  if constexpr (SCHED == 1) {
+    // activations split one K-tile ahead (b planes double-buffered in
+    // registers): the split of tile kt+1 and the loads of tile kt+2 run
+    // under the MFMAs of tile kt; the loop is unrolled by two so the two
+    // plane sets alternate without register copies
+    bf16x8 bA[3][TF], bB[3][TF];
+    load_w(0);
+    load_x(0);
+    put_w(0);
+    load_w(1);
+    split_x(bA);
+    load_x(1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    auto step = [&](int kt, bf16x8 (&b)[3][TF], bf16x8 (&bn)[3][TF]) {
+      const char *st = smem + (kt & 1) * STAGE;
+      bf16x8 a[3][TW];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+        for (int i = 0; i < TW; ++i) a[pl][i] = *reinterpret_cast<const bf16x8 *>(st + (pl * BW + i * 16) * 64 + foff);
+#pragma unroll
+      for (int i = 0; i < TW; ++i)
+#pragma unroll
+        for (int j = 0; j < TF; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TW; ++i)
+#pragma unroll
+        for (int j = 0; j < TF; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[0][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[1][j], acc[i][j], 0, 0, 0);
+        }
+#pragma unroll
+      for (int i = 0; i < TW; ++i)
+#pragma unroll
+        for (int j = 0; j < TF; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[2][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2][i], b[0][j], acc[i][j], 0, 0, 0);
+        }
+      split_x(bn);
+      load_x(kt + 2);
+      put_w(kt + 1);
+      load_w(kt + 2);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    };
+    int kt = 0;
+    for (; kt + 1 < ktiles; kt += 2) {
+      step(kt, bA, bB);
+      step(kt + 1, bB, bA);
+    }
+    if (kt < ktiles) step(kt, bA, bB);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    x6_epilogue<TW, TF, false>(p, acc, n0, fw, lane);
+    return;
+  }
+  load_w(0);
+  load_x(0);
+  put_w(0);
+  load_w(1);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < ktiles; ++kt) {
+    const char *st = smem + (kt & 1) * STAGE;
+    bf16x8 a[3][TW], b[3][TF];
+    split_x(b);
+    load_x(kt + 1);
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+      for (int i = 0; i < TW; ++i) a[pl][i] = *reinterpret_cast<const bf16x8 *>(st + (pl * BW + i * 16) * 64 + foff);
+#pragma unroll
+    for (int i = 0; i < TW; ++i)
+#pragma unroll
+      for (int j = 0; j < TF; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < TW; ++i)
+#pragma unroll
+      for (int j = 0; j < TF; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[1][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[0][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[1][j], acc[i][j], 0, 0, 0);
+      }
+#pragma unroll
+    for (int i = 0; i < TW; ++i)
+#pragma unroll
+      for (int j = 0; j < TF; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[2][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2][i], b[0][j], acc[i][j], 0, 0, 0);
+      }
+    put_w(kt + 1);
+    load_w(kt + 2);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  x6_epilogue<TW, TF, false>(p, acc, n0, fw, lane);
+}
+
+// Weight planes by LDS-DMA, activations in registers (gemm_bf16x6v_kernel):
+// the X6W geometry, but the weights arrive as the load-time bf16 planes
+// (GemmLayer::wsplit, n x 3 kpad) by global_load_lds into a 4-stage ring
+// issued three K-tiles ahead -- no VGPRs, no VALU, no ds_write for them --
+// and every wave's activation rows are loaded two K-tiles ahead into a
+// register double buffer and split in registers.  One barrier per K-tile,
+// at its top: this wave's pieces of tile kt and its rows of tile kt have
+// landed (counted vmcnt), so after the barrier every wave's have, and every
+// wave has finished reading the stage the next DMA overwrites.
+// Same products and accumulation order: bit-identical to the other kernels.
+template <class C>
+__global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6v_kernel(X6Args p) {
+  constexpr int BW = C::BW, TW = C::TW, TF = C::TF, NW = C::NW, STAGE = C::STAGE;
+  constexpr int NS = 4;                    // weight stages (DMA three K-tiles ahead)
+  constexpr int PIECES = 3 * (BW / 16);    // 1-KB DMA pieces per K-tile (16 rows x 64 B of one plane)
+  constexpr int PPW = PIECES / NW;         // pieces per wave
+  constexpr int XOPS = 2 * TF;             // activation loads per lane and K-tile
+  static_assert(PIECES % NW == 0, "pieces per wave");
+  static_assert(NS * STAGE <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef const __attribute__((address_space(1))) f32x4v gvec;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int tm, tn;
+  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
+  const int f0 = tm * C::BF, n0 = tn * BW;
+  const int ktiles = p.kpad / 32;
+  const int fw = f0 + wave * (TF * 16);
+  const int kq = (lane >> 4) * 8;
+
+  // this lane's source byte offset (at k = 0) and LDS offset for each of its
+  // wave's DMA pieces; chunk swizzle c ^ 2((r >> 3) & 1) on the source side
+  uint32_t dsrc[PPW];
+  int ddst[PPW];
+#pragma unroll
+  for (int t = 0; t < PPW; ++t) {
+    const int q = wave * PPW + t, plane = q / (BW / 16), rg = q % (BW / 16);
+    const int row = rg * 16 + (lane >> 2), chunk = (lane & 3) ^ (((row >> 3) & 1) << 1);
+    dsrc[t] = (uint32_t)((min(n0 + row, p.n - 1) * 3 * p.pw + plane * p.pw + chunk * 8) * 2);
+    ddst[t] = (plane * BW + rg * 16) * 64;
+  }
+  auto dma_w = [&](int kt) {
+    const int kc = min(kt, ktiles - 1);
+    char *st = smem + (kt % NS) * STAGE;
+    const char *wb = reinterpret_cast<const char *>(p.w) + kc * 64;
+#pragma unroll
+    for (int t = 0; t < PPW; ++t) glds16(wb + dsrc[t], st + ddst[t]);
+  };
+  const int din = p.din, mlast = p.m - 1, ldx = p.ldx;
+  const uint64_t offs = p.off_packed;
+  const float *xf = p.xf;
+  auto load_x = [&](int kt, f32x4v (&r0)[TF], f32x4v (&r1)[TF]) {
+    kt = min(kt, ktiles - 1);
+    const int k0 = kt * 32;
+    const int seg = k0 / din, col0 = k0 - seg * din;
+    const int shift = (int)(signed char)(offs >> (8 * seg));
+    gvec *xb = (gvec *)(xf + col0 + kq);
+#pragma unroll
+    for (int j = 0; j < TF; ++j) {
+      const int src = clampi(fw + j * 16 + (lane & 15) + shift, 0, mlast);
+      const uint32_t o = (uint32_t)(src * ldx) / 4;
+      r0[j] = xb[o];
+      r1[j] = xb[o + 1];
+    }
+  };
+  auto split_x = [&](const f32x4v (&r0)[TF], const f32x4v (&r1)[TF], bf16x8 (&b)[3][TF]) {
+#pragma unroll
+    for (int j = 0; j < TF; ++j) {
+      const Planes2 q0 = split3_pair(r0[j].x, r0[j].y), q1 = split3_pair(r0[j].z, r0[j].w);
+      const Planes2 q2 = split3_pair(r1[j].x, r1[j].y), q3 = split3_pair(r1[j].z, r1[j].w);
+      b[0][j] = __builtin_bit_cast(bf16x8, (u32x4{q0.h, q1.h, q2.h, q3.h}));
+      b[1][j] = __builtin_bit_cast(bf16x8, (u32x4{q0.m, q1.m, q2.m, q3.m}));
+      b[2][j] = __builtin_bit_cast(bf16x8, (u32x4{q0.l, q1.l, q2.l, q3.l}));
+    }
+  };
+
+  const int foff = (lane & 15) * 64 + (((lane >> 4) ^ (((lane >> 3) & 1) << 1)) * 16);
+  f32x4 acc[TW][TF];
+#pragma unroll
+  for (int i = 0; i < TW; ++i)
+#pragma unroll
+    for (int j = 0; j < TF; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+
+  f32x4v xa0[TF], xa1[TF], xb0[TF], xb1[TF];
+  // issue order DMA(0) DMA(1) X(0) DMA(2) X(1), then per step DMA(kt+3)
+  // X(kt+2): before every step the ops issued after X(kt) are one DMA group
+  // and one row group, so one counted wait covers W(kt) and X(kt)
+  dma_w(0);
+  dma_w(1);
+  load_x(0, xa0, xa1);
+  dma_w(2);
+  load_x(1, xb0, xb1);
+  auto step = [&](int kt, f32x4v (&r0)[TF], f32x4v (&r1)[TF]) {
+    wait_vmcnt<PPW + XOPS>();
+    __builtin_amdgcn_s_barrier();
+    bf16x8 b[3][TF];
+    split_x(r0, r1, b);
+    // keep the DMA issue behind the split (the compiler would hoist it and
+    // then wait for it with vmcnt(0) before the split)
+    __builtin_amdgcn_sched_barrier(0);
+    dma_w(kt + 3);
+    load_x(kt + 2, r0, r1);
+    const char *st = smem + (kt % NS) * STAGE;
+    bf16x8 a[3][TW];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+      for (int i = 0; i < TW; ++i) a[pl][i] = *reinterpret_cast<const bf16x8 *>(st + (pl * BW + i * 16) * 64 + foff);
+#pragma unroll
+    for (int i = 0; i < TW; ++i)
+#pragma unroll
+      for (int j = 0; j < TF; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < TW; ++i)
+#pragma unroll
+      for (int j = 0; j < TF; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[1][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[0][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[1][j], acc[i][j], 0, 0, 0);
+      }
+#pragma unroll
+    for (int i = 0; i < TW; ++i)
+#pragma unroll
+      for (int j = 0; j < TF; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[2][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2][i], b[0][j], acc[i][j], 0, 0, 0);
+      }
+  };
+  int kt = 0;
+  for (; kt + 1 < ktiles; kt += 2) {
+    step(kt, xa0, xa1);
+    step(kt + 1, xb0, xb1);
+  }
+  if (kt < ktiles) step(kt, xa0, xa1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  x6_epilogue<TW, TF, false>(p, acc, n0, fw, lane);
 }
 
 // Register-staged schedule: operands travel global -> VGPR (plain
@@ -1579,12 +2053,32 @@ int launch_z(hipStream_t s, X6Args p, bool out16) {
   return CE_GPU_OK;
 }
 
-template <class C, int SCHED = 0>
+template <class C, int SCHED = 0, int DIAG = 0>
 int launch_f(hipStream_t s, X6Args p) {
   p.tiles_n = (p.n + C::BW - 1) / C::BW;
   p.tiles_m = (p.m + C::BF - 1) / C::BF;
   dim3 grid(p.tiles_m * p.tiles_n), block(C::NT);
-  hipLaunchKernelGGL((gemm_bf16x6f_kernel<C, SCHED>), grid, block, 0, s, p);
+  hipLaunchKernelGGL((gemm_bf16x6f_kernel<C, SCHED, DIAG>), grid, block, 0, s, p);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
+template <class C, int SCHED = 0>
+int launch_w(hipStream_t s, X6Args p) {
+  p.tiles_n = (p.n + C::BW - 1) / C::BW;
+  p.tiles_m = (p.m + C::BF - 1) / C::BF;
+  dim3 grid(p.tiles_m * p.tiles_n), block(C::NT);
+  hipLaunchKernelGGL((gemm_bf16x6w_kernel<C, SCHED>), grid, block, 0, s, p);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
+template <class C>
+int launch_v(hipStream_t s, X6Args p) {
+  p.tiles_n = (p.n + C::BW - 1) / C::BW;
+  p.tiles_m = (p.m + C::BF - 1) / C::BF;
+  dim3 grid(p.tiles_m * p.tiles_n), block(C::NT);
+  hipLaunchKernelGGL((gemm_bf16x6v_kernel<C>), grid, block, 0, s, p);
   CE_HIP(hipGetLastError());
   return CE_GPU_OK;
 }
@@ -1722,6 +2216,45 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
         return launch_f<X6Cfg<128, 128, 2, 4, 2>, 6>(s, p);
       case 57:
         return launch_f<X6Cfg<256, 128, 4, 2, 2>, 6>(s, p);
+      case 59:
+        return launch_f<X6Cfg<128, 256, 2, 4, 2>, 7>(s, p);
+      // weights in LDS, activations in registers
+      case 170:
+        return launch_w<X6WCfg<128, 256, 8>>(s, p);
+      case 171:
+        return launch_w<X6WCfg<128, 128, 8>>(s, p);
+      case 172:
+        return launch_w<X6WCfg<64, 256, 8>>(s, p);
+      case 173:
+        return launch_w<X6WCfg<128, 256, 8>, 1>(s, p);
+      case 174:
+        return launch_w<X6WCfg<128, 128, 8>, 1>(s, p);
+      // weight planes by LDS-DMA, activations in registers
+      case 180:
+        return launch_v<X6WCfg<128, 256, 8>>(s, p);
+      case 181:
+        return launch_v<X6WCfg<128, 128, 8>>(s, p);
+      // ablations of 55 (wrong results: timing only)
+      case 91:
+        return launch_f<X6Cfg<128, 256, 2, 4, 2>, 6, 1>(s, p);
+      case 92:
+        return launch_f<X6Cfg<128, 256, 2, 4, 2>, 6, 2>(s, p);
+      case 94:
+        return launch_f<X6Cfg<128, 256, 2, 4, 2>, 6, 4>(s, p);
+      case 96:
+        return launch_f<X6Cfg<128, 256, 2, 4, 2>, 6, 16>(s, p);
+      case 98:
+        return launch_f<X6Cfg<128, 256, 2, 4, 2>, 6, 8>(s, p);
+      case 99:
+        return launch_f<X6Cfg<128, 256, 2, 4, 2>, 6, 3>(s, p);
+      case 100:
+        return launch_f<X6Cfg<128, 256, 2, 4, 2>, 6, 27>(s, p);
+      case 101:
+        return launch_f<X6Cfg<128, 256, 2, 4, 2>, 6, 59>(s, p);
+      case 102:
+        return launch_f<X6Cfg<128, 256, 2, 4, 2>, 6, 32>(s, p);
+      case 103:
+        return launch_f<X6Cfg<128, 256, 2, 4, 2>, 6, 43>(s, p);
       // 32x32x16 MFMA kernels; odd = weights from the load-time planes
       case 60:
         return launch_m<X6MCfg<128, 256, 2, 4>, false>(s, p);
@@ -1761,8 +2294,8 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
         return launch_c<X6CCfg<128, 256, 2, 4, 32>, false, 3>(s, p);
       case 42:  // round-1 default: split of tile kt+1, then the MFMAs of tile kt
         return launch_f<X6Cfg<128, 256, 2, 4, 2>>(s, p);
-      default:  // = 55
-        return launch_f<X6Cfg<128, 256, 2, 4, 2>, 6>(s, p);
+      default:  // = 160: region-scheduled loop
+        return launch_f<X6Cfg<128, 256, 2, 4, 2>, 8>(s, p);
     }
   }
   switch (x6_variant()) {
