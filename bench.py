@@ -189,6 +189,28 @@ def pmc_traffic(kernel, workload="c3"):
     return None, None
 
 
+def pmc_mfma(kernel, workload="c3"):
+    """Matrix-pipe utilisation of `kernel` from the newest committed
+    rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE summary
+    (tools/pmc_mfma.py over a serial run of this bench and workload): the
+    rocprof MFMA-utilisation figure the north star asks for, beside the
+    event-timed roofline fraction.  None if there is none."""
+    import glob
+    pattern = "r*_pmc_mfma.json" if workload == "c3" else f"r*_{workload}_pmc_mfma.json"
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", pattern))
+                   if workload != "c3" or not re.search(r"_c\d_pmc_mfma\.json$", f))
+    if not files:
+        return None
+    data = json.load(open(files[-1]))
+    for name, v in data.get("kernels", {}).items():
+        if name.endswith(kernel):
+            return {"chip": v["mfma_util_chip"], "active_cus": v["mfma_util_active_cus"],
+                    "source": os.path.relpath(files[-1], ROOT),
+                    "definition": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 x SIMDs), serial run: chip = "
+                                  "1024 SIMDs, active_cus = 4 x the CUs the grid occupies"}
+    return None
+
+
 def device_for_rank():
     """LOCAL_RANK's GPU; CATEARS_BENCH_DEVICE pins every rank to one device
     (rehearsing N ranks on a one-GPU box with --dist-backend gloo)."""
@@ -502,7 +524,8 @@ def main():
                         "traffic": traffic, "traffic_source": src,
                         "kernel": I8_ROOFLINE_KERNEL + " (TDNN-S layers 1-7)",
                         "launches": n, "avg_launch_ms": round(ms / n, 4), "busy_ms": round(busy, 3),
-                        "effective_ms_per_launch": round(busy / n, 4), "ops_per_launch": ops_per_launch}
+                        "effective_ms_per_launch": round(busy / n, 4), "ops_per_launch": ops_per_launch,
+                        "pmc_mfma_util": pmc_mfma(I8_ROOFLINE_KERNEL, "c5")}
         elif n and split:
             # split-plane GEMM: every Linear (layer 1 included) is one launch
             # of class GEMM.  `achieved` counts the algorithmic fp32 FLOPs
@@ -534,6 +557,7 @@ def main():
                         "launches": n, "avg_launch_ms": round(ms / n, 4), "busy_ms": round(busy, 3),
                         "effective_ms_per_launch": round(busy / n, 4),
                         "flops_per_launch": flops_per_launch,
+                        "pmc_mfma_util": pmc_mfma(kname),
                         "algorithmic_bytes_per_launch": split_algorithmic_bytes(plan.max_chunk_rows, eb),
                         "traffic_scope": ("PMC bytes per launch averaged over all 7 layers (fp32 operands)" if f32in else
                                           "PMC bytes per hidden-layer launch (split-output instantiation, layers "
@@ -556,6 +580,7 @@ def main():
                         "launches": n, "avg_launch_ms": round(ms / n, 4), "busy_ms": round(busy, 3),
                         "effective_ms_per_launch": round(busy / n, 4),
                         "flops_per_launch": flops_per_launch,
+                        "pmc_mfma_util": pmc_mfma(ROOFLINE_KERNEL),
                         "algorithmic_bytes_per_launch": gemm_algorithmic_bytes(plan.max_chunk_rows)}
         for name, (ms, n, busy) in prof.items():
             if n:

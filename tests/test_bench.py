@@ -42,3 +42,16 @@ def test_roofline_kernels_have_committed_traffic(bench, workload, kernel):
     traffic, src = bench.pmc_traffic(name, workload)
     assert src is not None, f"no committed PMC summary for {workload}"
     assert traffic is not None and traffic > 0, f"{name} not in {src}"
+
+
+@pytest.mark.parametrize("workload,kernel", [
+    ("c3", "SPLIT_BF16X6"),
+    ("c5", "I8"),
+])
+def test_roofline_kernels_have_committed_mfma_util(bench, workload, kernel):
+    """The rocprof MFMA-utilisation figure (north star) exists for the
+    dominant GEMM of C3 and C5 and is a fraction."""
+    name = bench.SPLIT_ROOFLINE_KERNEL["bf16x6"] if kernel == "SPLIT_BF16X6" else bench.I8_ROOFLINE_KERNEL
+    u = bench.pmc_mfma(name, workload)
+    assert u is not None, f"no committed MFMA-utilisation summary for {name} ({workload})"
+    assert 0.0 < u["chip"] <= u["active_cus"] <= 1.0

@@ -18,5 +18,6 @@ for W in "" _c2 _c5; do
 bench JSON line of the same command: profiles/${TAG}${W}_bench.json
 " > "$P/${TAG}${W}_kernel_summary.txt"
   [ -f "$S/pmc_traffic${W}.json" ] && cp "$S/pmc_traffic${W}.json" "$P/${TAG}${W}_pmc_traffic.json"
+  [ -f "$S/pmc_mfma${W}.json" ] && cp "$S/pmc_mfma${W}.json" "$P/${TAG}${W}_pmc_mfma.json"
 done
 ls -la "$P" | grep "$TAG"

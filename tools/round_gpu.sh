@@ -26,6 +26,11 @@ for grp in FETCH_SIZE WRITE_SIZE; do
   echo "pmc pass $i ok: $grp"
 done
 python "$R/tools/pmc_traffic.py" "$OUT/pmc1" "$OUT/pmc2" "$OUT/pmc_traffic.json"
+timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "gemm_" \
+    --output-format csv -d "$OUT/pmc3" -o run -- \
+    python "$R/bench.py" --steps 4 --warmup 1 --no-cpu-baseline --no-profile --serial \
+    > "$OUT/pmc3.log" 2>&1 || { echo "pmc pass 3 failed"; tail -20 "$OUT/pmc3.log"; exit 1; }
+python "$R/tools/pmc_mfma.py" "$OUT/pmc3" "$OUT/pmc_mfma.json"
 [ -n "$SKIP_EXTRA" ] && exit 0
 # secondary workloads: C2 (batched fbank) and C5 (int8 nnet), same recipe
 for W in c2 c5; do
@@ -41,4 +46,11 @@ for W in c2 c5; do
         > "$OUT/pmc_${W}_$i.log" 2>&1 || { echo "pmc $W $i failed"; tail -20 "$OUT/pmc_${W}_$i.log"; exit 1; }
   done
   python "$R/tools/pmc_traffic.py" "$OUT/pmc_${W}_1" "$OUT/pmc_${W}_2" "$OUT/pmc_traffic_$W.json"
+  if [ $W = c5 ]; then
+    timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "gemm_" \
+        --output-format csv -d "$OUT/pmc_${W}_3" -o run -- \
+        python "$R/bench.py" --workload $W --steps 3 --warmup 1 --no-cpu-baseline --no-profile --serial \
+        > "$OUT/pmc_${W}_3.log" 2>&1 || { echo "pmc $W 3 failed"; tail -20 "$OUT/pmc_${W}_3.log"; exit 1; }
+    python "$R/tools/pmc_mfma.py" "$OUT/pmc_${W}_3" "$OUT/pmc_mfma_$W.json"
+  fi
 done
