@@ -30,7 +30,7 @@ all: $(LIB) oracle
 $(OBJ)/gemm_bf16x6.o $(OBJ)/gemm_f16x3.o: HIPFLAGS += -mllvm -disable-promote-alloca-to-lds=1
 # no SLP-packed v_pk_add_f32 beside MFMAs (MI355X_MICROARCH.md: packed f32
 # VALU costs more issue cycles than the scalar pair in an MFMA gap)
-$(OBJ)/gemm_bf16x6.o: HIPFLAGS += -fno-slp-vectorize
+$(OBJ)/gemm_bf16x6.o: HIPFLAGS += -fno-slp-vectorize $(X6FLAGS)
 
 $(OBJ)/%.o: $(SRC)/kernels/%.hip $(HDRS)
 	@mkdir -p $(OBJ)
