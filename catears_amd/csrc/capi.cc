@@ -702,6 +702,12 @@ int ce_gpu_ctx_overflow(ce_gpu_ctx *ctx, int *overflow) {
   return CE_GPU_OK;
 }
 
+int ce_gpu_ctx_set_latency(ce_gpu_ctx *ctx, int on) {
+  if (!ctx) return fail(CE_GPU_EINVAL, "NULL argument");
+  ctx->latency = on ? 1 : 0;
+  return CE_GPU_OK;
+}
+
 int ce_gpu_ctx_synchronize(ce_gpu_ctx *ctx) {
   if (!ctx) return fail(CE_GPU_EINVAL, "ctx is NULL");
   CE_HIP(hipStreamSynchronize(ctx->stream));
@@ -1092,6 +1098,24 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
   CE_TRY(ensure_workspace(ctx, 2 * blk + (size_t)rows * m->num_pdfs));
   float *buf[2] = {ctx->workspace.as<float>(), ctx->workspace.as<float>() + blk};
   float *out = ctx->workspace.as<float>() + 2 * blk;
+  // latency mode: split-K slices per layer depend on K only (so results do
+  // not depend on the row count); workspace for the partials and tickets
+  auto slices = [](int kpad) { return std::max(1, std::min(8, kpad / 32 / 12)); };
+  if (ctx->latency) {
+    size_t part = 0, tickets = 0;
+    for (size_t i = 0; i < m->steps.size(); ++i) {
+      const GemmLayer &g = m->steps[i].gemm;
+      const int kpad = i == 0 ? g.kpad : g.nseg * g.din;
+      part = std::max(part, x6_split_part_floats(rows, g.n, slices(kpad)));
+      tickets = std::max(tickets, x6_split_tiles(rows, g.n));
+    }
+    if (ctx->split_part.bytes < part * sizeof(float) || ctx->split_ticket.bytes < tickets * sizeof(unsigned)) {
+      CE_HIP(hipStreamSynchronize(ctx->stream));  // the old buffers may still be in use
+      CE_TRY(ctx->split_part.alloc(part * sizeof(float)));
+      CE_TRY(ctx->split_ticket.alloc(tickets * sizeof(unsigned)));
+      CE_HIP(hipMemsetAsync(ctx->split_ticket.ptr, 0, tickets * sizeof(unsigned), ctx->stream));
+    }
+  }
   const float *xs = nullptr;
   int px = 0, cur = 0;
   ProfChain chain(ctx);  // every step below is one launch; GEMMs back to back
@@ -1129,6 +1153,12 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
     const int pn = (g.n + 31) / 32 * 32;
     a.y32 = last ? out : buf[cur];
     a.ldy = last ? g.n : pn;
+    if (ctx->latency) {
+      a.splitk = slices(a.kpad);
+      a.part = ctx->split_part.as<float>();
+      a.ticket = ctx->split_ticket.as<unsigned>();
+      a.split_tiles = ctx->split_ticket.bytes / sizeof(unsigned);
+    }
     {
       ProfScope prof(ctx, CE_GPU_PROF_GEMM);
       CE_TRY(launch_gemm_bf16x6(ctx->stream, a));

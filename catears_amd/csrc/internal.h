@@ -224,6 +224,9 @@ struct ce_gpu_ctx {
   catears::DevBuf scratch;     // reductions / int8 operand staging (grown on demand)
   catears::DevBuf blk_maps;    // ce_gpu_nnet_propagate_blocks: row_dst + row_edge
   catears::DevBuf overflow;    // int: an f16x3 split left the fp16 range (ce_gpu_ctx_overflow)
+  int latency = 0;             // ce_gpu_ctx_set_latency: split-K GEMMs for small batches
+  catears::DevBuf split_part;  // latency mode: GEMM partials (grown on demand)
+  catears::DevBuf split_ticket;  // latency mode: per-tile arrival counters (zeroed when grown)
   std::vector<int32_t> h_blk_maps;
   // optional per-class launch timing (ce_gpu_ctx_profile)
   bool profiling = false;
@@ -354,8 +357,17 @@ struct X6Gemm {
   float *y32 = nullptr;
   uint16_t *y16 = nullptr;
   int ldy = 0, py = 0;
+  // latency mode (fp32 operands): K split over `splitk` blocks per output
+  // tile, partials in `part` (x6_split_part_floats), one zeroed ticket per
+  // tile (at least x6_split_tiles); the sum over slices is in slice order
+  int splitk = 1;
+  float *part = nullptr;
+  unsigned *ticket = nullptr;
+  size_t split_tiles = 0;
 };
 int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a);
+size_t x6_split_part_floats(int m, int n, int splitk);
+size_t x6_split_tiles(int m, int n);
 // splice_pad (below) written as three bf16 planes of width po: out row r at
 // out + r * 3 * po.
 int launch_splice_pad_split(hipStream_t s, const float *in, int ld_in, int rows, int din, int nseg, const int *off,

@@ -53,6 +53,7 @@ namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2t __attribute__((ext_vector_type(2)));
 
 struct X6Args {
   const uint16_t *w;  // weights, n x ldw, plane stride pw (elements)
@@ -67,6 +68,9 @@ struct X6Args {
   int post[4];
   int npost, post_mode;
   int tiles_m, tiles_n, group;
+  float *part;       // split-K (latency mode): fp32 partials, splitk per tile
+  unsigned *ticket;  // split-K: arrival counter per tile, zero between launches
+  int splitk;
 };
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
@@ -352,9 +356,12 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6q_kernel(X6Args p) {
 // 2 = no global loads after the prologue, 4 = no MFMAs, 8 = no fragment
 // reads after the first tile, 16 = no K-tile barrier, 32 = no plane writes
 // after the prologue.
-template <class C, int SCHED, int DIAG = 0>
+// SPLIT (latency mode, SCHED 0 only): the K-tiles are split over p.splitk
+// blocks per output tile (see the fix-up after the loop).
+template <class C, int SCHED, int DIAG = 0, bool SPLIT = false>
 __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
   constexpr int BW = C::BW, BF = C::BF, TW = C::TW, TF = C::TF, NT = C::NT, STAGE = C::STAGE;
+  static_assert(!SPLIT || SCHED == 0, "split-K runs in the SCHED 0 loop");
   constexpr int RPP = NT / 4;  // rows per pass (4 threads x 32 B per row)
   static_assert(BW % RPP == 0 && BF % RPP == 0, "rows per pass");
   constexpr int NPW = BW / RPP, NPX = BF / RPP;
@@ -365,8 +372,18 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ww = wave / C::WGF, wf = wave % C::WGF;
+  // split-K: block b = 8 S q + 8 h + r computes K-slice h of tile 8 q + r
+  // (the slices of a tile share an XCD under round-robin dispatch: speed
+  // only); the grid is padded to whole groups of 8 S blocks
+  int tile = blockIdx.x, slice = 0;
+  if constexpr (SPLIT) {
+    const int g = 8 * p.splitk, rem = blockIdx.x % g;
+    slice = rem >> 3;
+    tile = (blockIdx.x / g) * 8 + (rem & 7);
+    if (tile >= p.tiles_m * p.tiles_n) return;
+  }
   int tm, tn;
-  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
+  tile_of(tile, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
   const int f0 = tm * BF, n0 = tn * BW;
   const int prow = tid >> 2, pch = tid & 3;
 
@@ -374,7 +391,12 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
   uint32_t wsrc[NPW];  // float offset of this thread's weight row at k = 0
 #pragma unroll
   for (int i = 0; i < NPW; ++i) wsrc[i] = (uint32_t)(min(n0 + prow + i * RPP, p.n - 1) * p.ldw + 8 * pch);
-  const int ktiles = p.kpad / 32;
+  int kbeg = 0, ktiles = p.kpad / 32;  // this block's K-tiles: kbeg .. ktiles-1
+  if constexpr (SPLIT) {
+    const int per = (ktiles + p.splitk - 1) / p.splitk;
+    kbeg = min(slice * per, ktiles);
+    ktiles = min(kbeg + per, ktiles);
+  }
   f32x4v rw0[NPW], rw1[NPW], rx0[NPX], rx1[NPX];
   auto load = [&](int kt) {
     if constexpr ((DIAG & 2) != 0) {
@@ -433,9 +455,9 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
 #pragma unroll
     for (int j = 0; j < TF; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 
-  load(0);
-  store(0);
-  load(1);
+  load(kbeg);
+  store(kbeg);
+  load(kbeg + 1);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if constexpr (SCHED >= 6) {
@@ -583,7 +605,7 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
     x6_epilogue<TW, TF, false>(p, acc, n0 + wrow, f0 + frow, lane);
     return;
   }
-  for (int kt = 0; kt < ktiles; ++kt) {
+  for (int kt = kbeg; kt < ktiles; ++kt) {
     store(kt + 1);
     load(kt + 2);
     const char *st = smem + (kt & 1) * STAGE;
@@ -620,6 +642,57 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
     __builtin_amdgcn_s_barrier();
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (SPLIT) {
+    // Last-arriver fix-up (MI355X_MICROARCH.md, inter-workgroup hand-offs,
+    // the table's first row, one block per CU): every slice publishes its
+    // fp32 partial in the accumulator layout with 8-B agent-scope stores
+    // (write-through, sc1), each wave drains them (vmcnt(0)), the block
+    // barrier, then one agent-scope add on the tile's ticket; the block whose
+    // add returns S-1 reads the other slices' partials with 8-B agent-scope
+    // loads and sums all S in slice order -- the same value whichever slice
+    // arrives last -- and runs the epilogue; the others exit.  No release
+    // fence (it would write back the XCD's dirty L2) and no wave ever waits
+    // on another block.
+    constexpr int WF4 = TW * TF * 64;  // f32x4 per wave and slice
+    typedef unsigned long long u64;
+    u64 *base = reinterpret_cast<u64 *>(p.part) + 2 * ((size_t)tile * p.splitk * C::NW * WF4 + wave * WF4 + lane);
+    const size_t sstride = 2 * (size_t)C::NW * WF4;  // u64 per slice
+#pragma unroll
+    for (int i = 0; i < TW; ++i)
+#pragma unroll
+      for (int j = 0; j < TF; ++j) {
+        u64 *d = base + slice * sstride + 2 * 64 * (i * TF + j);
+        const f32x4 v = acc[i][j];
+        __hip_atomic_store(d, __builtin_bit_cast(u64, (f32x2t{v[0], v[1]})), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(d + 1, __builtin_bit_cast(u64, (f32x2t{v[2], v[3]})), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __shared__ unsigned s_arrived;
+    __syncthreads();
+    if (tid == 0)
+      s_arrived = __hip_atomic_fetch_add(p.ticket + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (s_arrived != (unsigned)p.splitk - 1) return;
+    if (tid == 0) __hip_atomic_store(p.ticket + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+    f32x4 sum[TW][TF];
+    for (int h = 0; h < p.splitk; ++h) {
+#pragma unroll
+      for (int i = 0; i < TW; ++i)
+#pragma unroll
+        for (int j = 0; j < TF; ++j) {
+          f32x4 v = acc[i][j];
+          if (h != slice) {
+            const u64 *src = base + h * sstride + 2 * 64 * (i * TF + j);
+            const f32x2t lo = __builtin_bit_cast(f32x2t, __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            const f32x2t hi = __builtin_bit_cast(f32x2t, __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            v = f32x4{lo[0], lo[1], hi[0], hi[1]};
+          }
+          sum[i][j] = h == 0 ? v : sum[i][j] + v;
+        }
+    }
+    x6_epilogue<TW, TF, false>(p, sum, n0 + wrow, f0 + frow, lane);
+    return;
+  }
 
   x6_epilogue<TW, TF, false>(p, acc, n0 + wrow, f0 + frow, lane);
 }
@@ -676,6 +749,28 @@ int launch_f(hipStream_t s, X6Args p) {
   CE_HIP(hipGetLastError());
   return CE_GPU_OK;
 }
+
+// Latency mode: split-K over a.splitk blocks per tile (a.part / a.ticket
+// from the caller's workspace, sized by x6_split_part_floats /
+// x6_split_tiles).
+template <class C>
+int launch_f_split(hipStream_t s, X6Args p, const X6Gemm &a) {
+  p.tiles_n = (p.n + C::BW - 1) / C::BW;
+  p.tiles_m = (p.m + C::BF - 1) / C::BF;
+  const int tiles = p.tiles_m * p.tiles_n;
+  if ((size_t)tiles > a.split_tiles || !a.part || !a.ticket)
+    return fail(CE_GPU_EINVAL, "gemm_bf16x6: split-K workspace too small");
+  p.part = a.part;
+  p.ticket = a.ticket;
+  p.splitk = a.splitk;
+  dim3 grid((tiles + 7) / 8 * 8 * a.splitk), block(C::NT);
+  hipLaunchKernelGGL((gemm_bf16x6f_kernel<C, 0, 0, true>), grid, block, 0, s, p);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
+// latency-mode tile: 128 units x 128 frames, 8 waves of 32 x 64
+typedef X6Cfg<128, 128, 4, 2, 2> X6LatCfg;
 
 int x6_variant() {
   static int v = [] {
@@ -739,7 +834,11 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
   p.npost = a.npost;
   p.post_mode = post_mode(a.post, a.npost);
   p.group = 8;
+  p.part = nullptr;
+  p.ticket = nullptr;
+  p.splitk = 1;
   const bool out16 = a.y16 != nullptr;
+  if (f32in && a.splitk > 1) return launch_f_split<X6LatCfg>(s, p, a);
   if (f32in) {
     switch (x6_variant()) {
       case 40:  // 128 x 128 tiles: fills all CUs on a 1024-wide layer (one batch at a time on an idle GPU)
@@ -775,6 +874,15 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
   }
   // plane operands (CATEARS_X6_F32IN=0 / CE_GPU_GEMM_BF16X6_PLANES)
   return launch_q<X6Cfg<128, 128, 4, 2, 3>, 0>(s, p, out16);
+}
+
+size_t x6_split_part_floats(int m, int n, int splitk) {
+  const size_t tiles = (size_t)((m + X6LatCfg::BF - 1) / X6LatCfg::BF) * ((n + X6LatCfg::BW - 1) / X6LatCfg::BW);
+  return tiles * splitk * X6LatCfg::BW * X6LatCfg::BF;
+}
+
+size_t x6_split_tiles(int m, int n) {
+  return (size_t)((m + X6LatCfg::BF - 1) / X6LatCfg::BF) * ((n + X6LatCfg::BW - 1) / X6LatCfg::BW);
 }
 
 int launch_splice_pad_split(hipStream_t s, const float *in, int ld_in, int rows, int din, int nseg, const int *off,

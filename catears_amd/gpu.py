@@ -30,7 +30,7 @@ ABI = [
     "ce_gpu_nnet_propagate", "ce_gpu_linear", "ce_gpu_splice", "ce_gpu_rowwise",
     "ce_gpu_profile_anchor", "ce_gpu_ctx_profile_intervals", "ce_gpu_model_quantize",
     "ce_gpu_nnet_propagate_blocks", "ce_gpu_loglik_gather", "ce_gpu_loglik_columns",
-    "ce_gpu_model_set_gemm", "ce_gpu_model_get_gemm", "ce_gpu_ctx_overflow",
+    "ce_gpu_model_set_gemm", "ce_gpu_model_get_gemm", "ce_gpu_ctx_overflow", "ce_gpu_ctx_set_latency",
 ]
 
 # ce_gpu_model_set_gemm modes
@@ -98,6 +98,7 @@ def lib():
         "ce_gpu_model_set_gemm": (ci, [vp, ci]),
         "ce_gpu_model_get_gemm": (ci, [vp, pi]),
         "ce_gpu_ctx_overflow": (ci, [vp, pi]),
+        "ce_gpu_ctx_set_latency": (ci, [vp, ci]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -140,6 +141,11 @@ class Context:
 
     def synchronize(self):
         check(lib().ce_gpu_ctx_synchronize(self.h))
+
+    def set_latency(self, on=True):
+        """Latency mode (ce_gpu_ctx_set_latency): split-K nnet GEMMs for small
+        row blocks scored one at a time."""
+        check(lib().ce_gpu_ctx_set_latency(self.h, int(bool(on))))
 
     def overflow(self):
         """True if an f16x3 GEMM met an out-of-range activation since the

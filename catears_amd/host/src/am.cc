@@ -95,6 +95,11 @@ Status AcousticModel::Read(const Configuration &conf) {
   if (rc != CE_GPU_OK) return Status::Corruption(util::Format("{}: {}", nnet_file, ce_gpu_last_error()));
   int pdfs = 0;
   ce_gpu_model_info(model_, nullptr, nullptr, &feat_dim_, &pdfs, nullptr, nullptr);
+  // streaming chunks are small row blocks: latency mode (split-K GEMMs,
+  // ce_gpu_ctx_set_latency) unless the config turns it off; the process-wide
+  // context follows the last model loaded
+  if (ce_gpu_ctx_set_latency(rt.ctx(), conf.GetIntegerOrElse("gpu_latency_mode", 1)) != CE_GPU_OK)
+    return Status::RuntimeError(util::Format("gpu_latency_mode: {}", ce_gpu_last_error()));
   batcher_.reset(new Batcher());
   batcher_->max_blocks = conf.GetIntegerOrElse("gpu_batch_streams", 1);
   batcher_->wait = std::chrono::microseconds(conf.GetIntegerOrElse("gpu_batch_wait_us", 200));

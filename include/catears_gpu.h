@@ -79,6 +79,17 @@ int ce_gpu_ctx_synchronize(ce_gpu_ctx *ctx);
  * call, and clears the word.  When set, the log-likelihoods computed through
  * ctx since the last call are not fp32-accurate. */
 int ce_gpu_ctx_overflow(ce_gpu_ctx *ctx, int *overflow);
+/* Latency mode (on = 1) for callers that score small batches one at a time
+ * -- the streaming AcousticModel::Process path (src/am.cc:115-142, a
+ * chunk_size + left + right row block per call) or one utterance per call.
+ * The fp32 nnet GEMMs of ctx (default bf16x6 mode) then split their K
+ * dimension over up to 8 blocks per output tile (8 for K >= 3072, 2 for
+ * K = 1024) so a small row block still spreads over the chip, and sum the
+ * slices in slice order: deterministic and independent of the row count, so
+ * propagate_blocks still returns each block exactly the rows it gets alone.
+ * Results differ from the default mode's only by fp32 summation order.  Off
+ * (0, the default) is the throughput mode for full 4096-row batches. */
+int ce_gpu_ctx_set_latency(ce_gpu_ctx *ctx, int on);
 
 /* Kernel timing for roofline reporting: while enabled, every launch of the
  * given kernel class is bracketed by a pair of HIP events on the context's

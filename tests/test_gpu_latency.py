@@ -1,0 +1,95 @@
+"""Latency mode (ce_gpu_ctx_set_latency): the fp32 nnet GEMMs split K over
+up to 8 blocks per output tile so a small row block -- the streaming
+AcousticModel::Process chunk (src/am.cc:115-142) or one utterance -- spreads
+over the chip.  Same bars as the default mode: log-likelihoods within 1e-4
+of the oracle, bit-identical across row segmentations and batchings (the
+slice count depends on K only and slices are summed in slice order), and
+deterministic run to run (the last-arriver fix-up never races)."""
+import numpy as np
+import pytest
+
+from test_gpu_parity import LOGLIK_TOL, bits, dev
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return torch
+
+
+@pytest.fixture(scope="module")
+def G():
+    from catears_amd import gpu
+    gpu.lib()
+    return gpu
+
+
+@pytest.fixture(scope="module")
+def lctx(torch, G):
+    c = G.Context(0)
+    c.set_latency(True)
+    return c
+
+
+def test_latency_s_vs_oracle(torch, G, lctx, oracle, s_config):
+    from catears_amd import formats, synth
+    am = formats.read_am(s_config)
+    model = G.Model(lctx, s_config)
+    assert model.gemm == "bf16x6"
+    fb = oracle.Fbank()
+    feats = [fb.compute(synth.pcm(700 + i, n)) for i, n in enumerate([48000, 9000])]
+    plan = G.Plan(lctx, [48000, 9000], model)
+    out = G.am_forward(lctx, model, plan, dev(torch, np.concatenate(feats))).cpu().numpy()
+    off = plan.frame_offsets
+    for u, x in enumerate(feats):
+        ref = oracle.am_whole(am, x, gemm=lambda a, w: a @ w)
+        assert np.abs(out[off[u]:off[u + 1]] - ref).max() <= LOGLIK_TOL
+    # the default (throughput) mode differs only by fp32 summation order
+    tctx = G.Context(0)
+    tmodel = G.Model(tctx, s_config)
+    tout = G.am_forward(tctx, tmodel, G.Plan(tctx, [48000, 9000], tmodel), dev(torch, np.concatenate(feats))).cpu().numpy()
+    assert np.abs(out - tout).max() <= LOGLIK_TOL / 2
+
+
+def test_latency_segmentation_and_blocks_exact(torch, G, lctx, oracle, xs_config):
+    """Row segmentation (max_rows) and batching of independent blocks
+    (propagate_blocks, the multi-stream AcousticModel batcher) change no bit."""
+    from catears_amd import synth
+    model = G.Model(lctx, xs_config)
+    fb = oracle.Fbank()
+    feats = [fb.compute(synth.pcm(720 + i, n)) for i, n in enumerate([48000, 16000, 30000])]
+    ns = [(len(x) - 1) * 160 + 400 for x in feats]
+    x = dev(torch, np.concatenate(feats))
+    outs = [G.am_forward(lctx, model, G.Plan(lctx, ns, model, max_rows=r), x).cpu().numpy()
+            for r in (4096, 333, 64)]
+    assert np.array_equal(bits(outs[0]), bits(outs[1]))
+    assert np.array_equal(bits(outs[0]), bits(outs[2]))
+    rng = np.random.default_rng(721)
+    ctxr = model.left + model.right
+    rows = [70, 123, 70, 501]
+    blocks = [rng.normal(9.0, 3.0, size=(r, 40)).astype(np.float32) for r in rows]
+    together = G.nnet_propagate_blocks(lctx, model, dev(torch, np.concatenate(blocks)), rows).cpu().numpy()
+    alone = np.concatenate([G.nnet_propagate(lctx, model, dev(torch, b)).cpu().numpy() for b in blocks])
+    assert together.shape == (sum(rows) - len(rows) * ctxr, 512)
+    assert np.array_equal(bits(together), bits(alone))
+
+
+def test_latency_streaming_chunks_deterministic(torch, G, lctx, oracle, s_config):
+    """The streaming shape -- 50-frame chunks plus 20 context rows through
+    TDNN-S, one call each, 40 calls -- gives identical bits every time (the
+    per-tile tickets re-arm) and matches the oracle."""
+    from catears_amd import formats
+    am = formats.read_am(s_config)
+    model = G.Model(lctx, s_config)
+    rng = np.random.default_rng(730)
+    chunk = rng.normal(0.0, 3.0, size=(70, 40)).astype(np.float32)
+    d = dev(torch, chunk)
+    first = G.nnet_propagate(lctx, model, d).cpu().numpy()
+    for _ in range(40):
+        again = G.nnet_propagate(lctx, model, d)
+    assert np.array_equal(bits(first), bits(again.cpu().numpy()))
+    want = oracle.nnet_propagate(am["layers"], chunk, gemm=lambda a, w: a @ w)
+    assert np.abs(first - want).max() <= LOGLIK_TOL

@@ -1,0 +1,46 @@
+"""Per-call latency of ce_gpu_nnet_propagate on TDNN-S (one stream, calls back
+to back, HIP events), default (throughput) mode vs latency mode
+(ce_gpu_ctx_set_latency): the streaming AcousticModel chunk (chunk_size 50 +
+20 context rows), a 250-frame chunk, one 10 s utterance (1018 rows) and the
+bench's 4072-row batch.   python tools/latency.py [calls]"""
+import json
+import os
+import sys
+import tempfile
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from catears_amd import gpu, synth  # noqa: E402
+
+
+def main(calls=200):
+    mdir = os.path.join(tempfile.gettempdir(), f"catears_bench_{os.getuid()}")
+    conf = synth.write_model(mdir, "tdnn-s")
+    res = {}
+    for mode in ("throughput", "latency"):
+        ctx = gpu.Context(0)
+        ctx.set_latency(mode == "latency")
+        model = gpu.Model(ctx, conf)
+        for rows in (70, 270, 1018, 4072):
+            x = torch.from_numpy(np.random.default_rng(rows).normal(0, 3, size=(rows, 40)).astype(np.float32)).cuda()
+            out = gpu.nnet_propagate(ctx, model, x)
+            for _ in range(20):
+                gpu.nnet_propagate(ctx, model, x, out=out)
+            torch.cuda.synchronize()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(calls):
+                gpu.nnet_propagate(ctx, model, x, out=out)
+            b.record()
+            torch.cuda.synchronize()
+            us = a.elapsed_time(b) * 1e3 / calls
+            frames = rows - model.left - model.right
+            res[f"{mode}/{rows}"] = {"us_per_call": round(us, 1), "frames_per_s": round(frames / us * 1e6)}
+            print(f"{mode:10s} rows {rows:5d}: {us:8.1f} us/call  {frames / us * 1e6 / 1e6:7.3f} M frames/s", flush=True)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else 200)
