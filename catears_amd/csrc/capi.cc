@@ -1100,7 +1100,7 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
   float *out = ctx->workspace.as<float>() + 2 * blk;
   // latency mode: split-K slices per layer depend on K only (so results do
   // not depend on the row count); workspace for the partials and tickets
-  auto slices = [](int kpad) { return std::max(1, std::min(8, kpad / 32 / 12)); };
+  auto slices = [](int kpad) { return std::max(1, std::min(8, kpad / 32 / 6)); };
   if (ctx->latency) {
     size_t part = 0, tickets = 0;
     for (size_t i = 0; i < m->steps.size(); ++i) {

@@ -83,8 +83,9 @@ int ce_gpu_ctx_overflow(ce_gpu_ctx *ctx, int *overflow);
  * -- the streaming AcousticModel::Process path (src/am.cc:115-142, a
  * chunk_size + left + right row block per call) or one utterance per call.
  * The fp32 nnet GEMMs of ctx (default bf16x6 mode) then split their K
- * dimension over up to 8 blocks per output tile (8 for K >= 3072, 2 for
- * K = 1024) so a small row block still spreads over the chip, and sum the
+ * dimension over up to 8 blocks per output tile (at least 6 K-tiles of 32
+ * each: 8 for K >= 1536, 5 for K = 1024) so a small row block still spreads
+ * over the chip, and sum the
  * slices in slice order: deterministic and independent of the row count, so
  * propagate_blocks still returns each block exactly the rows it gets alone.
  * Results differ from the default mode's only by fp32 summation order.  Off
