@@ -1100,13 +1100,19 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
   float *out = ctx->workspace.as<float>() + 2 * blk;
   // latency mode: split-K slices per layer depend on K only (so results do
   // not depend on the row count); workspace for the partials and tickets
-  auto slices = [](int kpad) { return std::max(1, std::min(8, kpad / 32 / 6)); };
+  // K-slices per tile: >= 6 K-tiles each, at most 8, and about 64 blocks
+  // for a single 128-row tile block (a streaming chunk): wide layers need
+  // fewer slices.  A function of the layer's K and N only.
+  auto slices = [](int kpad, int n) {
+    const int cols = (n + 127) / 128;
+    return std::max(1, std::min(std::min(8, kpad / 32 / 6), (64 + cols - 1) / cols));
+  };
   if (ctx->latency) {
     size_t part = 0, tickets = 0;
     for (size_t i = 0; i < m->steps.size(); ++i) {
       const GemmLayer &g = m->steps[i].gemm;
       const int kpad = i == 0 ? g.kpad : g.nseg * g.din;
-      part = std::max(part, x6_split_part_floats(rows, g.n, slices(kpad)));
+      part = std::max(part, x6_split_part_floats(rows, g.n, slices(kpad, g.n)));
       tickets = std::max(tickets, x6_split_tiles(rows, g.n));
     }
     if (ctx->split_part.bytes < part * sizeof(float) || ctx->split_ticket.bytes < tickets * sizeof(unsigned)) {
@@ -1154,7 +1160,7 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
     a.y32 = last ? out : buf[cur];
     a.ldy = last ? g.n : pn;
     if (ctx->latency) {
-      a.splitk = slices(a.kpad);
+      a.splitk = slices(a.kpad, a.n);
       a.part = ctx->split_part.as<float>();
       a.ticket = ctx->split_ticket.as<unsigned>();
       a.split_tiles = ctx->split_ticket.bytes / sizeof(unsigned);

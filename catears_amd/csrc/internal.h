@@ -368,6 +368,9 @@ struct X6Gemm {
 int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a);
 size_t x6_split_part_floats(int m, int n, int splitk);
 size_t x6_split_tiles(int m, int n);
+// latency-mode GEMMs run in launches of at most this many rows (bounds the
+// partial workspace: <= 16 x 27 tiles x 8 slices x 64 KB)
+constexpr int kX6SplitWindow = 2048;
 // splice_pad (below) written as three bf16 planes of width po: out row r at
 // out + r * 3 * po.
 int launch_splice_pad_split(hipStream_t s, const float *in, int ld_in, int rows, int din, int nseg, const int *off,

@@ -71,6 +71,7 @@ struct X6Args {
   float *part;       // split-K (latency mode): fp32 partials, splitk per tile
   unsigned *ticket;  // split-K: arrival counter per tile, zero between launches
   int splitk;
+  int row0;          // split-K: first row of this launch's row window
 };
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
@@ -375,16 +376,17 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
   // split-K: block b = 8 S q + 8 h + r computes K-slice h of tile 8 q + r
   // (the slices of a tile share an XCD under round-robin dispatch: speed
   // only); the grid is padded to whole groups of 8 S blocks
-  int tile = blockIdx.x, slice = 0;
+  int tile = blockIdx.x, slice = 0, row0 = 0;
   if constexpr (SPLIT) {
     const int g = 8 * p.splitk, rem = blockIdx.x % g;
     slice = rem >> 3;
     tile = (blockIdx.x / g) * 8 + (rem & 7);
+    row0 = p.row0;  // this launch's row window (tiles_m covers the window only)
     if (tile >= p.tiles_m * p.tiles_n) return;
   }
   int tm, tn;
   tile_of(tile, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
-  const int f0 = tm * BF, n0 = tn * BW;
+  const int f0 = row0 + tm * BF, n0 = tn * BW;
   const int prow = tid >> 2, pch = tid & 3;
 
   typedef const __attribute__((address_space(1))) f32x4v gvec;
@@ -753,19 +755,26 @@ int launch_f(hipStream_t s, X6Args p) {
 // Latency mode: split-K over a.splitk blocks per tile (a.part / a.ticket
 // from the caller's workspace, sized by x6_split_part_floats /
 // x6_split_tiles).
+// One launch per window of kX6SplitWindow rows (whole tiles), so the
+// partial workspace stays bounded for long blocks; tiles never straddle a
+// window, so the results do not depend on the windowing.
 template <class C>
 int launch_f_split(hipStream_t s, X6Args p, const X6Gemm &a) {
+  static_assert(kX6SplitWindow % C::BF == 0, "window of whole tiles");
   p.tiles_n = (p.n + C::BW - 1) / C::BW;
-  p.tiles_m = (p.m + C::BF - 1) / C::BF;
-  const int tiles = p.tiles_m * p.tiles_n;
-  if ((size_t)tiles > a.split_tiles || !a.part || !a.ticket)
-    return fail(CE_GPU_EINVAL, "gemm_bf16x6: split-K workspace too small");
   p.part = a.part;
   p.ticket = a.ticket;
   p.splitk = a.splitk;
-  dim3 grid((tiles + 7) / 8 * 8 * a.splitk), block(C::NT);
-  hipLaunchKernelGGL((gemm_bf16x6f_kernel<C, 0, 0, true>), grid, block, 0, s, p);
-  CE_HIP(hipGetLastError());
+  for (int r0 = 0; r0 < p.m; r0 += kX6SplitWindow) {
+    p.row0 = r0;
+    p.tiles_m = (std::min(kX6SplitWindow, p.m - r0) + C::BF - 1) / C::BF;
+    const int tiles = p.tiles_m * p.tiles_n;
+    if ((size_t)tiles > a.split_tiles || !a.part || !a.ticket)
+      return fail(CE_GPU_EINVAL, "gemm_bf16x6: split-K workspace too small");
+    dim3 grid((tiles + 7) / 8 * 8 * a.splitk), block(C::NT);
+    hipLaunchKernelGGL((gemm_bf16x6f_kernel<C, 0, 0, true>), grid, block, 0, s, p);
+    CE_HIP(hipGetLastError());
+  }
   return CE_GPU_OK;
 }
 
@@ -837,6 +846,7 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
   p.part = nullptr;
   p.ticket = nullptr;
   p.splitk = 1;
+  p.row0 = 0;
   const bool out16 = a.y16 != nullptr;
   if (f32in && a.splitk > 1) return launch_f_split<X6LatCfg>(s, p, a);
   if (f32in) {
@@ -876,13 +886,13 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
   return launch_q<X6Cfg<128, 128, 4, 2, 3>, 0>(s, p, out16);
 }
 
-size_t x6_split_part_floats(int m, int n, int splitk) {
-  const size_t tiles = (size_t)((m + X6LatCfg::BF - 1) / X6LatCfg::BF) * ((n + X6LatCfg::BW - 1) / X6LatCfg::BW);
-  return tiles * splitk * X6LatCfg::BW * X6LatCfg::BF;
+size_t x6_split_tiles(int m, int n) {
+  m = std::min(m, kX6SplitWindow);
+  return (size_t)((m + X6LatCfg::BF - 1) / X6LatCfg::BF) * ((n + X6LatCfg::BW - 1) / X6LatCfg::BW);
 }
 
-size_t x6_split_tiles(int m, int n) {
-  return (size_t)((m + X6LatCfg::BF - 1) / X6LatCfg::BF) * ((n + X6LatCfg::BW - 1) / X6LatCfg::BW);
+size_t x6_split_part_floats(int m, int n, int splitk) {
+  return x6_split_tiles(m, n) * splitk * X6LatCfg::BW * X6LatCfg::BF;
 }
 
 int launch_splice_pad_split(hipStream_t s, const float *in, int ld_in, int rows, int din, int nseg, const int *off,

@@ -84,8 +84,9 @@ int ce_gpu_ctx_overflow(ce_gpu_ctx *ctx, int *overflow);
  * chunk_size + left + right row block per call) or one utterance per call.
  * The fp32 nnet GEMMs of ctx (default bf16x6 mode) then split their K
  * dimension over up to 8 blocks per output tile (at least 6 K-tiles of 32
- * each: 8 for K >= 1536, 5 for K = 1024) so a small row block still spreads
- * over the chip, and sum the
+ * each, and about 64 blocks for one 128-row tile block: TDNN-S 8 slices for
+ * its 3072 x 1024 layers, 5 for 1024 x 1024, 2 for 1024 x 3456) so a small
+ * row block still spreads over the chip, and sum the
  * slices in slice order: deterministic and independent of the row count, so
  * propagate_blocks still returns each block exactly the rows it gets alone.
  * Results differ from the default mode's only by fp32 summation order.  Off

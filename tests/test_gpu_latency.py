@@ -93,3 +93,24 @@ def test_latency_streaming_chunks_deterministic(torch, G, lctx, oracle, s_config
     assert np.array_equal(bits(first), bits(again.cpu().numpy()))
     want = oracle.nnet_propagate(am["layers"], chunk, gemm=lambda a, w: a @ w)
     assert np.abs(first - want).max() <= LOGLIK_TOL
+
+
+def test_latency_long_block_windows(torch, G, lctx, oracle, xs_config):
+    """A block longer than the split-K row window (2048 rows) runs in several
+    launches: the same bits as scoring two overlapping halves separately,
+    and the oracle's values around a window seam."""
+    from catears_amd import formats
+    am = formats.read_am(xs_config)
+    model = G.Model(lctx, xs_config)
+    ctx_rows = model.left + model.right
+    rows = 5000
+    x = np.random.default_rng(740).normal(9.0, 3.0, size=(rows, 40)).astype(np.float32)
+    dx = dev(torch, x)
+    got = G.nnet_propagate(lctx, model, dx).cpu().numpy()
+    cut = 3000
+    a = G.nnet_propagate(lctx, model, dx[:cut + ctx_rows]).cpu().numpy()
+    b = G.nnet_propagate(lctx, model, dx[cut:]).cpu().numpy()
+    assert np.array_equal(bits(got), bits(np.concatenate([a, b])))
+    lo, hi = 2048 - 30, 2048 + 30
+    want = oracle.nnet_propagate(am["layers"], x[lo:hi + ctx_rows])
+    assert np.abs(got[lo:hi] - want).max() <= LOGLIK_TOL
