@@ -758,9 +758,11 @@ int launch_f(hipStream_t s, X6Args p) {
 // One launch per window of kX6SplitWindow rows (whole tiles), so the
 // partial workspace stays bounded for long blocks; tiles never straddle a
 // window, so the results do not depend on the windowing.
-template <class C>
+template <class C, int PAD = 0>
 int launch_f_split(hipStream_t s, X6Args p, const X6Gemm &a) {
   static_assert(kX6SplitWindow % C::BF == 0, "window of whole tiles");
+  // PAD: dynamic LDS that keeps the block alone on its CU (the write-through
+  // hand-off above is the measured one-block-per-CU form)
   p.tiles_n = (p.n + C::BW - 1) / C::BW;
   p.part = a.part;
   p.ticket = a.ticket;
@@ -772,14 +774,21 @@ int launch_f_split(hipStream_t s, X6Args p, const X6Gemm &a) {
     if ((size_t)tiles > a.split_tiles || !a.part || !a.ticket)
       return fail(CE_GPU_EINVAL, "gemm_bf16x6: split-K workspace too small");
     dim3 grid((tiles + 7) / 8 * 8 * a.splitk), block(C::NT);
-    hipLaunchKernelGGL((gemm_bf16x6f_kernel<C, 0, 0, true>), grid, block, 0, s, p);
+    hipLaunchKernelGGL((gemm_bf16x6f_kernel<C, 0, 0, true>), grid, block, PAD, s, p);
     CE_HIP(hipGetLastError());
   }
   return CE_GPU_OK;
 }
 
-// latency-mode tile: 128 units x 128 frames, 8 waves of 32 x 64
+// latency-mode tiles: 128 units x 128 frames, 8 waves of 32 x 64; for row
+// blocks of at most kX6LatSmallRows (a streaming chunk) 128 x 64, 4 waves of
+// 64 x 32 (72 KB of LDS, padded to one block per CU).  The tile shape does
+// not change any output bit (same K-tile and product order per element,
+// slices by K and N only).
 typedef X6Cfg<128, 128, 4, 2, 2> X6LatCfg;
+typedef X6Cfg<128, 64, 2, 2, 2> X6LatSmallCfg;
+constexpr int kX6LatSmallRows = 256;
+constexpr int kX6LatSmallPad = 82 * 1024 - 2 * X6LatSmallCfg::STAGE;
 
 int x6_variant() {
   static int v = [] {
@@ -848,7 +857,9 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
   p.splitk = 1;
   p.row0 = 0;
   const bool out16 = a.y16 != nullptr;
-  if (f32in && a.splitk > 1) return launch_f_split<X6LatCfg>(s, p, a);
+  if (f32in && a.splitk > 1)
+    return a.m <= kX6LatSmallRows ? launch_f_split<X6LatSmallCfg, kX6LatSmallPad>(s, p, a)
+                                  : launch_f_split<X6LatCfg>(s, p, a);
   if (f32in) {
     switch (x6_variant()) {
       case 40:  // 128 x 128 tiles: fills all CUs on a 1024-wide layer (one batch at a time on an idle GPU)
@@ -888,11 +899,20 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
 
 size_t x6_split_tiles(int m, int n) {
   m = std::min(m, kX6SplitWindow);
-  return (size_t)((m + X6LatCfg::BF - 1) / X6LatCfg::BF) * ((n + X6LatCfg::BW - 1) / X6LatCfg::BW);
+  const size_t cols = (n + X6LatCfg::BW - 1) / X6LatCfg::BW;
+  const size_t big = (m + X6LatCfg::BF - 1) / X6LatCfg::BF * cols;
+  const size_t small = m <= kX6LatSmallRows ? (m + X6LatSmallCfg::BF - 1) / X6LatSmallCfg::BF * cols : 0;
+  return std::max(big, small);
 }
 
 size_t x6_split_part_floats(int m, int n, int splitk) {
-  return x6_split_tiles(m, n) * splitk * X6LatCfg::BW * X6LatCfg::BF;
+  m = std::min(m, kX6SplitWindow);
+  const size_t cols = (n + X6LatCfg::BW - 1) / X6LatCfg::BW;
+  const size_t big = (m + X6LatCfg::BF - 1) / X6LatCfg::BF * cols * X6LatCfg::BW * X6LatCfg::BF;
+  const size_t small = m <= kX6LatSmallRows
+                           ? (m + X6LatSmallCfg::BF - 1) / X6LatSmallCfg::BF * cols * X6LatSmallCfg::BW * X6LatSmallCfg::BF
+                           : 0;
+  return std::max(big, small) * splitk;
 }
 
 int launch_splice_pad_split(hipStream_t s, const float *in, int ld_in, int rows, int din, int nseg, const int *off,
