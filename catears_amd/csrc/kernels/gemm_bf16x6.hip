@@ -699,6 +699,150 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
   x6_epilogue<TW, TF, false>(p, acc, n0 + wrow, f0 + frow, lane);
 }
 
+// Warp-specialised fp32-in schedule: the block is C::NW MFMA waves plus
+// NPV producer waves.  The producers do all the global loads, splits and
+// plane writes of tile kt+1 while the MFMA waves read and multiply tile kt,
+// so the split VALU issues in the cycles the matrix pipe leaves free on the
+// same SIMD instead of between a wave's own MFMAs.  Same LDS stages, layout,
+// product order and per-K-tile barrier as gemm_bf16x6f_kernel's SCHED 0 loop
+// (bit-identical results):
+//   WAR: stage (kt+1) % 2 was read in step kt-1, whose reads were drained
+//        (lgkmcnt(0)) before the barrier closing it;
+//   RAW: the producers' writes of tile kt+1 are drained before the barrier
+//        closing step kt, and the MFMA waves read them after it.
+// Both roles pass the same number of barriers (one prologue + one per K-tile;
+// the role test is wave-uniform, readfirstlane).  Producer rows: the stage's
+// BW weight rows then BF activation rows, 4 threads x 32 B per row, pass i
+// covering rows i RPP .. i RPP + RPP - 1 (a pass may straddle the two kinds:
+// per-thread selects).  Measured against the default: DESIGN.md §8.
+template <class C, int NPV>
+__global__ __launch_bounds__(C::NT + 64 * NPV, 1) void gemm_bf16x6ws_kernel(X6Args p) {
+  constexpr int BW = C::BW, BF = C::BF, TW = C::TW, TF = C::TF, NT = C::NT, STAGE = C::STAGE;
+  constexpr int RPP = 16 * NPV;  // producer rows per pass
+  static_assert((BW + BF) % RPP == 0, "rows per pass");
+  constexpr int NP = (BW + BF) / RPP;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  auto swz = [](int row) { return ((row >> 3) & 1) << 1; };
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef const __attribute__((address_space(1))) f32x4v gvec;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int tm, tn;
+  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
+  const int f0 = tm * BF, n0 = tn * BW;
+  const int ktiles = p.kpad / 32;
+
+  if (wave >= C::NW) {  // producer
+    const int pt = tid - NT, prow = pt >> 2, pch = pt & 3;
+    bool isw[NP];
+    int trow[NP];         // row within its plane block
+    uint32_t wsrc[NP];    // weight rows: float offset at k = 0
+    int dst[NP];          // byte offset of the chunk in the stage
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int r = i * RPP + prow;
+      isw[i] = BW % RPP == 0 ? i < BW / RPP : r < BW;  // compile-time when no pass straddles
+      trow[i] = isw[i] ? r : r - BW;
+      wsrc[i] = (uint32_t)(min(n0 + trow[i], p.n - 1) * p.ldw + 8 * pch);
+      dst[i] = (isw[i] ? 0 : 3 * BW * 64) + trow[i] * 64 + ((pch ^ swz(trow[i])) * 16);
+    }
+    f32x4v r0[NP], r1[NP];
+    auto load = [&](int kt) {
+      kt = min(kt, ktiles - 1);
+      const int k0 = kt * 32;
+      const int seg = k0 / p.din, col0 = k0 - seg * p.din;
+      const int shift = (int)(signed char)(p.off_packed >> (8 * seg));
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        gvec *src;
+        if (isw[i]) {
+          src = (gvec *)(p.wf + k0 + wsrc[i]);
+        } else {
+          const int x = clampi(f0 + trow[i] + shift, 0, p.m - 1);
+          src = (gvec *)(p.xf + (uint32_t)(x * p.ldx) + col0 + 8 * pch);
+        }
+        r0[i] = src[0];
+        r1[i] = src[1];
+      }
+    };
+    auto store = [&](int kt) {
+      char *st = smem + (kt & 1) * STAGE;
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        const f32x4v v0 = r0[i], v1 = r1[i];
+        const Planes2 q0 = split3_pair(v0.x, v0.y), q1 = split3_pair(v0.z, v0.w);
+        const Planes2 q2 = split3_pair(v1.x, v1.y), q3 = split3_pair(v1.z, v1.w);
+        const int ps = (isw[i] ? BW : BF) * 64;  // plane stride in the stage
+        char *d = st + dst[i];
+        *reinterpret_cast<u32x4 *>(d) = u32x4{q0.h, q1.h, q2.h, q3.h};
+        *reinterpret_cast<u32x4 *>(d + ps) = u32x4{q0.m, q1.m, q2.m, q3.m};
+        *reinterpret_cast<u32x4 *>(d + 2 * ps) = u32x4{q0.l, q1.l, q2.l, q3.l};
+      }
+    };
+    load(0);
+    store(0);
+    load(1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    for (int kt = 0; kt < ktiles; ++kt) {
+      store(kt + 1);  // past the end: the clamped last tile into a stage no step reads
+      load(kt + 2);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+  }
+
+  // MFMA waves
+  const int ww = wave / C::WGF, wf = wave % C::WGF;
+  const int foff = (lane & 15) * 64 + (((lane >> 4) ^ (((lane >> 3) & 1) << 1)) * 16);
+  const int wrow = ww * TW * 16, frow = wf * TF * 16;
+  f32x4 acc[TW][TF];
+#pragma unroll
+  for (int i = 0; i < TW; ++i)
+#pragma unroll
+    for (int j = 0; j < TF; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < ktiles; ++kt) {
+    const char *st = smem + (kt & 1) * STAGE;
+    bf16x8 a[3][TW], b[3][TF];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+      for (int i = 0; i < TW; ++i)
+        a[pl][i] = *reinterpret_cast<const bf16x8 *>(st + (pl * BW + wrow + i * 16) * 64 + foff);
+#pragma unroll
+      for (int j = 0; j < TF; ++j)
+        b[pl][j] = *reinterpret_cast<const bf16x8 *>(st + 3 * BW * 64 + (pl * BF + frow + j * 16) * 64 + foff);
+    }
+#pragma unroll
+    for (int i = 0; i < TW; ++i)
+#pragma unroll
+      for (int j = 0; j < TF; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[0][j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < TW; ++i)
+#pragma unroll
+      for (int j = 0; j < TF; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[1][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[0][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1][i], b[1][j], acc[i][j], 0, 0, 0);
+      }
+#pragma unroll
+    for (int i = 0; i < TW; ++i)
+#pragma unroll
+      for (int j = 0; j < TF; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0][i], b[2][j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2][i], b[0][j], acc[i][j], 0, 0, 0);
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  x6_epilogue<TW, TF, false>(p, acc, n0 + wrow, f0 + frow, lane);
+}
+
 // First layer: the spliced, zero-padded block (splice_pad_kernel's output)
 // written directly as three bf16 planes.  out row r = [plane0 | plane1 |
 // plane2], each `po` wide; columns nseg*din .. po-1 are zero.
@@ -748,6 +892,16 @@ int launch_f(hipStream_t s, X6Args p) {
   p.tiles_m = (p.m + C::BF - 1) / C::BF;
   dim3 grid(p.tiles_m * p.tiles_n), block(C::NT);
   hipLaunchKernelGGL((gemm_bf16x6f_kernel<C, SCHED, DIAG>), grid, block, 0, s, p);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
+template <class C, int NPV>
+int launch_ws(hipStream_t s, X6Args p) {
+  p.tiles_n = (p.n + C::BW - 1) / C::BW;
+  p.tiles_m = (p.m + C::BF - 1) / C::BF;
+  dim3 grid(p.tiles_m * p.tiles_n), block(C::NT + 64 * NPV);
+  hipLaunchKernelGGL((gemm_bf16x6ws_kernel<C, NPV>), grid, block, 0, s, p);
   CE_HIP(hipGetLastError());
   return CE_GPU_OK;
 }
@@ -868,6 +1022,12 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
         return launch_f<X6Cfg<128, 256, 2, 4, 2>>(s, p);
       case 55:  // MFMAs of tile kt first, the split interleaved by the compiler
         return launch_f<X6Cfg<128, 256, 2, 4, 2>, 6>(s, p);
+      case 200:  // warp-specialised: 4 MFMA waves (64 x 64 each) + 4 producer waves
+        return launch_ws<X6Cfg<128, 128, 2, 2, 2>, 4>(s, p);
+      case 202:  // 128 x 256: 4 MFMA waves of 64 x 128 + 4 producers
+        return launch_ws<X6Cfg<128, 256, 2, 2, 2>, 4>(s, p);
+      case 204:  // 128 x 256: 8 MFMA waves of 64 x 64 + 4 producers (3 waves per SIMD)
+        return launch_ws<X6Cfg<128, 256, 2, 4, 2>, 4>(s, p);
       // ablations of 55 (wrong results: timing only)
       case 91:
         return launch_f<X6Cfg<128, 256, 2, 4, 2>, 6, 1>(s, p);

@@ -1,0 +1,43 @@
+"""The opt-in bf16x6 GEMM schedules (CATEARS_X6_VARIANT, read once per
+process: one child process each) give the default's bits.  Every variant
+accumulates each output element over the same K-tiles in the same order with
+the same six products per tile, so the tile shape (128 x 128,
+variant 40), the round-1 loop order (42) and the warp-specialised producer /
+MFMA-wave split (200, 202, 204) must not change any bit of TDNN-S's output."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+CHILD = r"""
+import sys, numpy as np, torch
+from catears_amd import gpu
+ctx = gpu.Context(0)
+model = gpu.Model(ctx, sys.argv[1])
+assert model.gemm == "bf16x6", model.gemm
+x = np.random.default_rng(750).normal(9.0, 3.0, size=(3000, 40)).astype(np.float32)
+out = gpu.nnet_propagate(ctx, model, torch.from_numpy(x).to("cuda:0")).cpu().numpy()
+np.save(sys.argv[2], out)
+"""
+
+
+def _run(variant, cfg, path):
+    env = dict(os.environ, CATEARS_X6_VARIANT=str(variant), PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-c", CHILD, cfg, str(path)], env=env, capture_output=True, text=True,
+                       timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return np.load(path).view(np.uint32)
+
+
+def test_x6_variants_bit_identical(tmp_path, s_config):
+    base = _run(0, s_config, tmp_path / "v0.npy")
+    assert base.ndim == 2 and base.shape[0] > 0
+    for v in (40, 42, 200, 202, 204):
+        got = _run(v, s_config, tmp_path / f"v{v}.npy")
+        assert np.array_equal(got, base), f"variant {v} differs from the default"
