@@ -1103,9 +1103,18 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
   // K-slices per tile: >= 6 K-tiles each, at most 8, and about 64 blocks
   // for a single 128-row tile block (a streaming chunk): wide layers need
   // fewer slices.  A function of the layer's K and N only.
+  // (CATEARS_LAT_SLICES="min_ktiles,max_slices,target_blocks" overrides the
+  // rule for measurements)
+  static const int *rule = [] {
+    static int r[3] = {6, 8, 64};
+    if (const char *e = getenv("CATEARS_LAT_SLICES")) sscanf(e, "%d,%d,%d", &r[0], &r[1], &r[2]);
+    return r;
+  }();
   auto slices = [](int kpad, int n) {
-    const int cols = (n + 127) / 128;
-    return std::max(1, std::min(std::min(8, kpad / 32 / 6), (64 + cols - 1) / cols));
+    const int cols = (n + 127) / 128, kt = kpad / 32;
+    const int s = std::max(1, std::min(std::min(rule[1], kt / rule[0]), (rule[2] + cols - 1) / cols));
+    const int per = (kt + s - 1) / s;
+    return (kt + per - 1) / per;  // no empty slice
   };
   if (ctx->latency) {
     size_t part = 0, tickets = 0;
