@@ -49,39 +49,36 @@ CE_HD void fft_lane_op(uint32_t addr, uint32_t meta, const float *tw, float *re,
   const int p0 = (int)(addr & 255u), p1 = (int)((addr >> 8) & 255u);
   const int p2 = (int)((addr >> 16) & 255u), p3 = (int)(addr >> 24);
   float t1, t2;
-  if (kind == 3u) {  // length-2 node (srfft.cc:206-216)
-    t1 = re[p0] + re[p1]; re[p1] = re[p0] - re[p1]; re[p0] = t1;
-    t1 = im[p0] + im[p1]; im[p1] = im[p0] - im[p1]; im[p0] = t1;
-    return;
-  }
+  // every kind reads and writes its four slots here, so a generation that
+  // mixes kinds issues one set of LDS accesses (a length-2 op's slots are
+  // p0 p1 p0 p1: it writes its two results twice, the same values)
   float ar = re[p0], ai = im[p0], br = re[p1], bi = im[p1];
   float cr = re[p2], ci = im[p2], dr = re[p3], di = im[p3];
-  if (kind == 2u) {  // length-4 node (srfft.cc:163-205), points a b c d = 0 1 2 3
+  // The kinds share their steps (same operations, same order per value):
+  // a length-4 node is the general node's first two steps followed by the
+  // (a, b) butterfly instead of twiddles; a length-2 node is that butterfly
+  // alone.  Sharing them keeps a mixed generation's divergent paths short.
+  if (kind != 3u) {
+    // general node step 1 / length-4 (srfft.cc:163-205, points a b c d =
+    // 0 1 2 3): butterflies (n, n+h) and (n+q, n+q+h)
     t1 = ar + cr; cr = ar - cr; ar = t1;
     t1 = ai + ci; ci = ai - ci; ai = t1;
     t1 = br + dr; dr = br - dr; br = t1;
     t1 = bi + di; di = bi - di; bi = t1;
+    // step 2: (h+n, h+q+n) / the length-4 node's (c, d) rotation
+    t1 = cr + di;
+    t2 = ci + dr;
+    ci = ci - dr;
+    dr = cr - di;
+    cr = t1;
+    di = t2;
+  }
+  if (kind != 1u) {
+    // (a, b) butterfly of a length-4 node, or a length-2 node (srfft.cc:206-216)
     t1 = ar + br; br = ar - br; ar = t1;
     t1 = ai + bi; bi = ai - bi; ai = t1;
-    t1 = cr + di;
-    t2 = ci + dr;
-    ci = ci - dr;
-    dr = cr - di;
-    cr = t1;
-    di = t2;
-  } else {  // general node: this lane owns n, n+q, n+h, n+h+q
-    // step 1: butterflies (n, n+h) and (n+q, n+q+h)
-    t1 = ar + cr; cr = ar - cr; ar = t1;
-    t1 = ai + ci; ci = ai - ci; ai = t1;
-    t1 = br + dr; dr = br - dr; br = t1;
-    t1 = bi + di; di = bi - di; bi = t1;
-    // step 2: (h+n, h+q+n)
-    t1 = cr + di;
-    t2 = ci + dr;
-    ci = ci - dr;
-    dr = cr - di;
-    cr = t1;
-    di = t2;
+    if (kind == 3u) cr = ar, ci = ai, dr = br, di = bi;
+  } else {
     // steps 3 & 4: twiddles for n >= 1
     const uint32_t twc = (meta >> 2) & 3u;
     if (twc == 1u) {
@@ -156,6 +153,7 @@ CE_HD float mel_dot(const float *w, const float *p, int len) {
   for (int i = 0; i < len; ++i) e += w[i] * p[i];
   return e;
 }
+
 
 }  // namespace fb
 }  // namespace catears
