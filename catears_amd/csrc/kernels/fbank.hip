@@ -34,7 +34,7 @@ constexpr int kFramesPerBlock = 4;  // one wave per frame, 4 waves per block
 #ifndef FBANK_GENS
 #define FBANK_GENS kFftGens  // (timing experiments only may lower it)
 #endif
-constexpr int kBlocksPerCU = 5;     // residency of fbank_kernel (31 KB LDS, 82 VGPRs)
+constexpr int kBlocksPerCU = 5;     // residency of fbank_kernel (27 KB LDS, 96 VGPRs)
 constexpr int kMaxBlocks = 256 * kBlocksPerCU;
 
 __device__ __forceinline__ void wave_sync() {
@@ -69,7 +69,9 @@ struct BlockTables {
 // post-pass twiddles and LDS slots, the lane's mel band) -- then its four
 // waves walk frames f = 4 * block + wave, f += 4 * gridDim.x.  Per frame the
 // only global traffic is the 1.6 kB PCM read and the 160 B feature write.
-__global__ __launch_bounds__(256) void fbank_kernel(const FbankTables *__restrict__ tab,
+// 5 waves per SIMD (the LDS bound; unrolled, the compiler would otherwise
+// take 117 VGPRs and 4 waves)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) void fbank_kernel(const FbankTables *__restrict__ tab,
                                                     const float *__restrict__ pcm,
                                                     const int64_t *__restrict__ sample_off,
                                                     const int64_t *__restrict__ frame_off,
@@ -150,18 +152,13 @@ __global__ __launch_bounds__(256) void fbank_kernel(const FbankTables *__restric
     }
     wave_sync();
 
-    // 3. split-radix generations (the descriptors rotate through the
-    // registers: after kFftGens steps they are back in place for the next
-    // frame, and the loop stays rolled, keeping the register count low)
-#pragma unroll 1
+    // 3. split-radix generations, unrolled: each generation reads its own
+    // descriptor register (a rolled loop rotated the seven descriptors
+    // through the registers, 7 moves per generation: 2 % slower)
+#pragma unroll
     for (int g = 0; g < FBANK_GENS; ++g) {
       const int o = g * 64 + lane;
-      fb::fft_lane_op(gaddr[0], gmeta & 15u, bt.tw + 6 * o, S.re, S.im);
-      const uint32_t a0 = gaddr[0];
-#pragma unroll
-      for (int j = 0; j + 1 < kFftGens; ++j) gaddr[j] = gaddr[j + 1];
-      gaddr[kFftGens - 1] = a0;
-      gmeta = (gmeta >> 4) | ((gmeta & 15u) << (4 * (kFftGens - 1)));
+      fb::fft_lane_op(gaddr[g], (gmeta >> (4 * g)) & 15u, bt.tw + 6 * o, S.re, S.im);
       wave_sync();
     }
 
