@@ -5,17 +5,29 @@ ARCH ?= gfx950
 JOBS ?= 8
 
 SRC := catears_amd/csrc
+# EXPERIMENTS=1: the measurement build for tools/ -- every tuning variant and
+# the DIAG ablation kernels (wrong results, timing only) -- as a separate
+# library (point CATEARS_HIP_LIB at it).  The product library carries the
+# default kernels and the documented, bit-identical alternatives only.
+EXPERIMENTS ?= 0
+ifeq ($(EXPERIMENTS),1)
+OBJ := build/obj_exp
+LIB := catears_amd/lib/libcatears_hip_exp.so
+EXPFLAGS := -DCATEARS_EXPERIMENTS -DCATEARS_DIAG
+else
 OBJ := build/obj
 LIB := catears_amd/lib/libcatears_hip.so
+EXPFLAGS :=
+endif
 
 # -ffp-contract=off: the reference's float arithmetic is never fused
 # (x86-64 without FMA); keeping mul/add separate makes the fbank, CMVN and
 # epilogue arithmetic bit-identical to it.  MFMA accumulation is unaffected.
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off \
-            -Iinclude -I$(SRC) -Wall -Wno-unused-function
+            -Iinclude -I$(SRC) -Wall -Wno-unused-function $(EXPFLAGS)
 CXX ?= g++
 HOSTFLAGS := -O2 -fPIC -std=c++17 -ffp-contract=off -Iinclude -I$(SRC) -I/opt/rocm/include \
-             -D__HIP_PLATFORM_AMD__ -Wall
+             -D__HIP_PLATFORM_AMD__ -Wall $(EXPFLAGS)
 
 KERNELS := $(wildcard $(SRC)/kernels/*.hip)
 HOSTSRC := $(SRC)/capi.cc $(SRC)/tables.cc
@@ -24,6 +36,9 @@ OBJS := $(patsubst $(SRC)/kernels/%.hip,$(OBJ)/%.o,$(KERNELS)) \
 HDRS := include/catears_gpu.h $(SRC)/internal.h $(SRC)/fbank_ops.h $(SRC)/tile_order.h $(SRC)/lds_dma.h
 
 all: $(LIB) oracle
+
+# `make EXPERIMENTS=1 lib` builds only the measurement library
+lib: $(LIB)
 
 # the bf16x6 GEMM's small per-lane arrays stay in registers (hipcc would
 # otherwise promote one into LDS at 1 block/CU: +36 KB of LDS traffic)
@@ -48,10 +63,10 @@ oracle:
 	$(MAKE) -C oracle
 
 clean:
-	rm -rf build $(LIB) $(PKLIB) $(PKTEST)
+	rm -rf build $(LIB) catears_amd/lib/libcatears_hip_exp.so $(PKLIB) $(PKTEST)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all lib oracle clean
 
 # ---------------------------------------------------------------------------
 # Drop-in pocketkaldi classes (C++ host layer over the C-ABI).  compat/ holds

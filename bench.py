@@ -72,10 +72,19 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL) for real runs; gloo only to rehearse N ranks on one GPU "
                          "together with CATEARS_BENCH_DEVICE")
-    ap.add_argument("--workload", choices=["c3", "c2", "c5"], default="c3",
+    ap.add_argument("--workload", choices=["c3", "c2", "c4", "c5"], default="c3",
                     help="c3: full pipeline fp32 (the headline metric); c2: batched fbank only, "
-                         "1000 x 10 s utterances per step; c5: full pipeline with the int8 nnet path, "
-                         "frame batch 8192")
+                         "1000 x 10 s utterances per step; c4: the 100 h length-mixed corpus sharded over "
+                         "the ranks, one pass (steps = each rank's batches), ragged batches gathered to "
+                         "rank 0; c5: full pipeline with the int8 nnet path, frame batch 8192")
+    ap.add_argument("--c4-utts", type=int, default=36000,
+                    help="c4 corpus size in utterances (36000 = 100 h; smaller for tests)")
+    ap.add_argument("--c4-dump", default=None,
+                    help="c4, tests only: rank 0 writes every gathered row (and its own) per utterance "
+                         "to this .npz (small corpora)")
+    ap.add_argument("--pcm", choices=["f32", "s16"], default="f32",
+                    help="resident PCM format: f32 (raw int16 scale floats, WaveReader's output) or s16 "
+                         "(the WAV payload; ce_gpu_fbank_s16 converts exactly in the kernel)")
     ap.add_argument("--gemm", choices=["fp32", "bf16x6", "bf16x6p", "f16x3"], default=None,
                     help="matrix-core form of the fp32 Linear layers (ce_gpu_model_set_gemm); default: "
                          "the library's (bf16x6: three exact bf16 planes, six products, fp32 GEMM)")
@@ -85,6 +94,30 @@ def parse():
                     help="nnet streams; consecutive batches alternate between them so one batch's "
                          "wave-quantisation tail overlaps the next batch's layers")
     return ap.parse_args()
+
+
+def usable_cores():
+    """Host cores this process may run on: the CPU affinity set, capped by
+    the cgroup CPU quota (a GPU box's share of a larger machine: nproc and
+    os.cpu_count() report the whole machine there).  Returns (cores, how)."""
+    import math
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    if quota is not None and math.ceil(quota) < aff:
+        return max(1, int(math.floor(quota))), f"cgroup CPU quota {quota:g} of {aff} CPUs in the affinity set"
+    return aff, f"CPU affinity set ({aff} CPUs, no smaller cgroup quota)"
 
 
 def cpu_baseline(conf, n_utts, seconds, threads, min_wall):
@@ -271,9 +304,11 @@ def main_c2(args):
     stream = torch.cuda.current_stream()
     ctx = gpu.Context(local, stream)
     plan = gpu.Plan(ctx, [n_samp] * n_utt)
-    pcm = torch.empty((n_utt, n_samp), dtype=torch.float32, device="cuda")
+    s16 = args.pcm == "s16"
+    pcm = torch.empty((n_utt, n_samp), dtype=torch.int16 if s16 else torch.float32, device="cuda")
     for u in range(n_utt):
-        pcm[u].copy_(torch.from_numpy(synth.pcm(rank * 100003 + u, n_samp)))
+        w = synth.pcm(rank * 100003 + u, n_samp)
+        pcm[u].copy_(torch.from_numpy(w.astype(np.int16) if s16 else w))
     pcm = pcm.reshape(-1)
     feats = torch.empty((plan.total_frames, 40), dtype=torch.float32, device="cuda")
     for _ in range(args.warmup):
@@ -306,7 +341,7 @@ def main_c2(args):
             dist.destroy_process_group()
         return
     roofline = None
-    bytes_per_launch = 4 * n_utt * n_samp + 4 * 40 * plan.total_frames
+    bytes_per_launch = (2 if s16 else 4) * n_utt * n_samp + 4 * 40 * plan.total_frames
     if iv:
         avg_ms = sum(b - a for a, b in iv) / len(iv)
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
@@ -318,11 +353,13 @@ def main_c2(args):
                     "valu_flops_per_frame": 14000}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        threads = min(16, os.cpu_count() or 1)
-        v, fr, dt, passes = cpu_fbank_baseline(64, args.seconds, threads, args.cpu_seconds)
+        threads, how = usable_cores()
+        v, fr, dt, passes = cpu_fbank_baseline(max(64, 2 * threads), args.seconds, threads, args.cpu_seconds)
         cpu = {"value": round(v, 1), "unit": "frames/s", "cores": threads, "kind": "port",
-               "sample": f"{passes} passes over 64 x {args.seconds:g} s utterances ({fr} frames, {dt:.1f} s wall, "
-                         f"{threads} worker threads): oracle fbank (C restatement of src/fbank.cc + srfft.cc)"}
+               "per_core": round(v / threads, 1), "cores_basis": how,
+               "sample": f"{passes} passes over {max(64, 2 * threads)} x {args.seconds:g} s utterances ({fr} frames, "
+                         f"{dt:.1f} s wall, {threads} worker threads): oracle fbank (C restatement of src/fbank.cc "
+                         "+ srfft.cc)"}
     line = {
         "metric": "fbank frames/sec (window+SRFFT+mel+log, 25ms/10ms, 40 bins), 16kHz",
         "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
@@ -330,6 +367,7 @@ def main_c2(args):
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
         "data": "synthetic (seeded 16 kHz PCM at raw int16 scale)",
         "config": {"workload": f"C2 batched fbank only, {n_utt} x {args.seconds:g} s utterances per step per GPU",
+                   "pcm": "int16 (WAV payload)" if s16 else "float32 at raw int16 scale",
                    "frames_per_step_per_gpu": plan.total_frames, "parallelism": f"utterance shard x{world}"},
         "roofline": roofline, "cpu_baseline": cpu, "checksum": checksum,
     }
@@ -339,15 +377,255 @@ def main_c2(args):
         dist.destroy_process_group()
 
 
-def main():
-    args = parse()
-    if args.workload == "c2":
-        return main_c2(args)
+def main_c4(args):
+    """BASELINE.json config C4: the 100 h corpus (36 000 seeded 2-18 s
+    utterances, exactly 100 h of 16 kHz audio, catears_amd.shard.c4_corpus)
+    sharded over the ranks by shard_utterances (longest-first greedy by
+    frames), each rank packing its utterances into <= 4096-row batches and
+    scoring them through fbank -> CMVN -> TDNN-S -> -log prior with the C3
+    pipeline (one front and `back_streams` nnet streams).  Every rank's
+    log-likelihood batches -- ragged: their row counts are exchanged once at
+    setup -- stream to rank 0 over RCCL point-to-point (RowGather), where
+    every row is folded into a checksum.  The timed region is one pass over
+    the whole corpus (steps = the largest rank's batch count); PCM for every
+    utterance is resident in HBM before it starts.  value = all ranks' frames
+    / the slowest rank's time.  --c4-dump (tests) makes rank 0 keep every
+    row it consumed, per utterance."""
     import torch
     import torch.distributed as dist
 
     from catears_amd import gpu, synth
-    from catears_amd.shard import LoglikGather
+    from catears_amd.shard import RowGather, c4_corpus, exchange_counts, num_frames, pack_batches, shard_utterances
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = device_for_rank()
+    torch.cuda.set_device(local)
+    if world > 1:
+        init_dist(args, local)
+    mdir = os.path.join(tempfile.gettempdir(), f"catears_bench_{os.getuid()}")
+    if int(os.environ.get("LOCAL_RANK", 0)) == 0:
+        synth.write_model(mdir, args.model)
+    if world > 1:
+        dist.barrier()
+    conf = synth.write_model(mdir, args.model)
+
+    NB = 1 if args.serial else max(1, args.back_streams)
+    backs = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(NB - 1)]
+    front = backs[0] if args.serial else torch.cuda.Stream()
+    ctxs = [gpu.Context(local, b) for b in backs]
+    ctx_f = ctxs[0] if args.serial else gpu.Context(local, front)
+    model = gpu.Model(ctxs[0], conf)
+    if args.gemm:
+        model.set_gemm(args.gemm)
+    L, R, pdfs = model.left, model.right, model.num_pdfs
+
+    # corpus, shard, batches (all deterministic; the row counts are exchanged)
+    samples = c4_corpus(args.c4_utts)
+    frames = [num_frames(int(n)) for n in samples]
+    mine = shard_utterances(frames, world, rank)
+    batches = [[mine[i] for i in b] for b in pack_batches([frames[u] for u in mine], L, R, 4096)]
+    my_rows = [sum(frames[u] for u in b) for b in batches]
+    if world > 1:
+        everyone = exchange_counts([(b, r) for b, r in zip(batches, my_rows)])
+    else:
+        everyone = [list(zip(batches, my_rows))]
+    counts = [[r for _, r in e] for e in everyone]
+    steps = max(len(c) for c in counts)
+    frames_all = sum(sum(c) for c in counts)
+
+    # resident PCM: utterance u = the first n_u samples of pool signal u % P
+    # (content depends on the utterance only, not on the rank or batching)
+    P, plen = 48, int(samples.max())
+    pool_np = np.stack([synth.pcm(600000 + i, plen) for i in range(P)])
+    s16 = args.pcm == "s16"
+    pool = torch.from_numpy(pool_np.astype(np.int16) if s16 else pool_np).cuda()
+    tot = int(sum(int(samples[u]) for u in mine))
+    pcm = torch.empty(max(tot, 1), dtype=pool.dtype, device="cuda")
+    bstart, at = [], 0
+    for b in batches:
+        bstart.append(at)
+        for u in b:
+            n = int(samples[u])
+            pcm[at:at + n].copy_(pool[u % P, :n])
+            at += n
+    plans = [gpu.Plan(ctxs[0], [int(samples[u]) for u in b], model, max_rows=4096) for b in batches]
+    for pl, rows in zip(plans, my_rows):
+        assert pl.total_frames == rows
+    gstats = None if args.no_cmvn else torch.from_numpy(synth.cmvn_stats_synthetic()).cuda()
+    maxf = max(my_rows) if my_rows else 1
+    F = 2 * NB + 2 if not args.serial else 2
+    raw = [torch.empty((maxf, 40), dtype=torch.float32, device="cuda") for _ in range(F)]
+    norm = [torch.empty_like(raw[0]) for _ in range(F)] if gstats is not None else raw
+    ready = [torch.cuda.Event() for _ in range(F)]
+    free = [torch.cuda.Event() for _ in range(F)]
+    nbuf = max(3, NB + 1)
+    outs = [torch.empty((maxf, pdfs), dtype=torch.float32, device="cuda") for _ in range(nbuf)]
+    done = [None] * nbuf
+    gather = world > 1 and not args.no_gather
+    dump = {} if (args.c4_dump and rank == 0) else None
+    gat = RowGather(counts, pdfs, torch.float32, "cuda", depth=nbuf, keep=dump is not None) if gather else None
+    comm = torch.cuda.Stream() if gather else None
+    checksum = torch.zeros((), dtype=torch.float64, device="cuda")
+
+    def front_stage(i):
+        slot = i % F
+        front.wait_event(free[slot])
+        pl = plans[i]
+        src = pcm[bstart[i]:bstart[i] + pl.total_samples]
+        gpu.fbank(ctx_f, pl, src, raw[slot][:pl.total_frames])
+        if gstats is not None:
+            gpu.cmvn(ctx_f, pl, gstats, raw[slot][:pl.total_frames], norm[slot][:pl.total_frames])
+        ready[slot].record(front)
+
+    def back_stage(i, s, timed):
+        # i: this rank's batch, s: the gather step
+        slot, o, b = i % F, i % nbuf, i % NB
+        stream = backs[b]
+        if gat is not None and timed:
+            with torch.cuda.stream(stream):
+                gat.wait_slot(s % nbuf)
+        if done[o] is not None:
+            stream.wait_event(done[o])
+        stream.wait_event(ready[slot])
+        n = plans[i].total_frames
+        gpu.am_forward(ctxs[b], model, plans[i], norm[slot][:n], outs[o][:n])
+        free[slot].record(stream)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        done[o] = ev
+        if not timed:
+            return
+        if gat is not None:
+            with torch.cuda.stream(comm):
+                comm.wait_event(ev)
+                gat.submit(s, outs[o], own=outs[o][:n] if rank == 0 else None)
+        else:
+            # one process: consume every row the same way rank 0 does
+            with torch.cuda.stream(stream):
+                checksum.add_(torch.sum(outs[o][:n], dtype=torch.float64))
+        if dump is not None and (rank == 0):
+            stream.synchronize()
+            _c4_keep(dump, batches[i], frames, outs[o][:n].cpu().numpy())
+
+    def idle_step(s):
+        # this rank has no batch at step s but peers may (rank 0 receives)
+        if gat is not None:
+            with torch.cuda.stream(comm):
+                gat.submit(s, None)
+
+    # warm-up: the first W batches, scored untimed and not gathered
+    W = min(args.warmup, len(batches))
+    if W:
+        front_stage(0)
+        for i in range(W):
+            if i + 1 < W:
+                front_stage(i + 1)
+            back_stage(i, i, False)
+    torch.cuda.synchronize()
+    done = [None] * nbuf
+    if not args.no_profile:
+        gpu.profile_anchor(local, backs[0])
+        for c in set(ctxs + [ctx_f]):
+            c.profile(True, classes=[ctxs[0].PROF_GEMM])
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    if batches:
+        front_stage(0)
+    for s in range(steps):
+        if s < len(batches):
+            if s + 1 < len(batches):
+                front_stage(s + 1)
+            back_stage(s, s, True)
+        else:
+            idle_step(s)
+    if gat is not None:
+        with torch.cuda.stream(comm):
+            gat.drain()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if gat is not None:
+        checksum += gat.checksum
+    rows_in = gat.rows_in if gat is not None else 0
+    busy = None
+    n_gemm = 0
+    if not args.no_profile:
+        iv = []
+        for c in ctxs:
+            iv += c.profile_intervals(c.PROF_GEMM)
+            c.profile(False)
+        ctx_f.profile(False)
+        n_gemm = len(iv)
+        busy = gpu.union_ms(iv)
+    if dump is not None and gat is not None:
+        for p, st, rows in gat.keep:
+            _c4_keep(dump, everyone[p][st][0], frames, rows)
+    value = frames_all / elapsed
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+    if dump is not None:
+        np.savez(args.c4_dump, **{f"u{u}": a for u, a in dump.items()})
+    roofline = None
+    if busy:
+        peak = MFMA_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS.get(model.gemm, 1) if model.gemm != "fp32" else MFMA_F32_PEAK_TFLOPS
+        achieved = sum(counts[0]) * FLOPS_PER_FRAME / (busy * 1e-3) / 1e12  # rank 0's frames, rank 0's GEMMs
+        roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
+                    "frac": round(achieved / peak, 4), "traffic": None,
+                    "kernel": "rank 0's nnet GEMM launches (every TDNN-S Linear), union of their intervals",
+                    "launches": n_gemm, "busy_ms": round(busy, 3)}
+    line = {
+        "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world,
+        "steps": steps, "warmup": W, "ms_per_step": round(elapsed * 1e3 / max(steps, 1), 4),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": SPLIT_DTYPE.get(model.gemm, "fp32"),
+        "data": "synthetic (seeded 16 kHz PCM, random-init TDNN-S in NN02 format)",
+        "config": {"workload": f"C4 {args.c4_utts} x 2-18 s utterances ({int(samples.sum()) / 16000 / 3600:.3g} h), "
+                               f"utterance shard x{world}, <= 4096-row batches, fbank->CMVN->{args.model}->loglik, "
+                               + ("ragged log-likelihood batches gathered to rank 0 (RCCL p2p)" if gather else
+                                  "no gather"),
+                   "utterances": int(args.c4_utts), "frames_total": int(frames_all),
+                   "frames_per_rank": [int(sum(c)) for c in counts], "batches_per_rank": [len(c) for c in counts],
+                   "rows_gathered_to_rank0": int(rows_in), "pcm": args.pcm, "cmvn": not args.no_cmvn,
+                   "parallelism": f"utterance shard x{world}", "streams": 1 if args.serial else 1 + NB,
+                   "gather": gather},
+        "roofline": roofline, "cpu_baseline": None,
+        "checksum": float(checksum.item()),
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _c4_keep(dump, utts, frames, rows):
+    """Split a batch's rows (utterances back to back) per utterance."""
+    at = 0
+    for u in utts:
+        dump[int(u)] = rows[at:at + frames[u]]
+        at += frames[u]
+    assert at == rows.shape[0]
+
+
+def main():
+    args = parse()
+    if args.workload == "c2":
+        return main_c2(args)
+    if args.workload == "c4":
+        return main_c4(args)
+    import torch
+    import torch.distributed as dist
+
+    from catears_amd import gpu, synth
+    from catears_amd.shard import RowGather, exchange_counts
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
@@ -397,7 +675,8 @@ def main():
 
     # resident PCM pool (distinct utterances per rank)
     pool = max(args.pool, U)
-    pcm = torch.from_numpy(np.stack([synth.pcm(rank * 100003 + i, n_samp) for i in range(pool)])).cuda()
+    pcm_np = np.stack([synth.pcm(rank * 100003 + i, n_samp) for i in range(pool)])
+    pcm = torch.from_numpy(pcm_np.astype(np.int16) if args.pcm == "s16" else pcm_np).cuda()
     gstats = None if args.no_cmvn else torch.from_numpy(synth.cmvn_stats_synthetic()).cuda()
     # feature slots: NB being scored plus NB + 2 already featurised, so the
     # front stream runs a whole round of batches ahead and a stream that
@@ -414,7 +693,13 @@ def main():
             for _ in range(nbuf)]
     done = [None] * nbuf  # event: the batch that last wrote outs[o] has finished
     gather = world > 1 and not args.no_gather
-    gat = LoglikGather(outs[0].shape, torch.float32, "cuda", depth=nbuf) if gather else None
+    # every rank sends each of its batches (all rows) to rank 0, which folds
+    # every received row into a checksum; the per-step row counts are
+    # exchanged once here (equal at C3; C4's are ragged, main_c4)
+    gat = None
+    if gather:
+        counts = exchange_counts([frames_per_step] * (args.warmup + args.steps))
+        gat = RowGather(counts, model.num_pdfs, torch.float32, "cuda", depth=nbuf)
     comm = torch.cuda.Stream() if gather else None
     checksum = torch.zeros((), dtype=torch.float64, device="cuda")
 
@@ -446,12 +731,12 @@ def main():
         ev.record(stream)
         done[o] = ev
         if gat is not None:
-            # the collective is enqueued from a stream of its own that waits
+            # the transfer is enqueued from a stream of its own that waits
             # for this batch only, so the nnet streams never wait on each
             # other through it
             with torch.cuda.stream(comm):
                 comm.wait_event(ev)
-                assert gat.submit(outs[o]) == o
+                assert gat.submit(i, outs[o], own=outs[o] if rank == 0 else None) == o
 
     def run(first, count):
         front_stage(first)
@@ -482,9 +767,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     # the outputs are consumed (checksum) so no work can be elided
-    checksum += outs[(args.warmup + args.steps - 1) % nbuf].double().sum()
     if gat is not None:
         checksum += gat.checksum
+    else:
+        checksum += outs[(args.warmup + args.steps - 1) % nbuf].double().sum()
     finite = bool(torch.isfinite(outs[0]).all().item())
     # f16x3: no activation left the two-plane range in any batch
     overflow = any(c.overflow() for c in set(ctxs + ctx_fs))
@@ -606,10 +892,12 @@ def main():
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        threads = min(16, os.cpu_count() or 1)
-        v, fr, dt, passes = cpu_baseline(conf, args.cpu_utts, args.seconds, threads, args.cpu_seconds)
+        threads, how = usable_cores()
+        n_cpu = max(args.cpu_utts, 2 * threads)
+        v, fr, dt, passes = cpu_baseline(conf, n_cpu, args.seconds, threads, args.cpu_seconds)
         cpu = {"value": round(v, 1), "unit": "frames/s", "cores": threads, "kind": "port",
-               "sample": f"{passes} passes over {args.cpu_utts} x {args.seconds:g} s utterances ({fr} frames, "
+               "per_core": round(v / threads, 1), "cores_basis": how,
+               "sample": f"{passes} passes over {n_cpu} x {args.seconds:g} s utterances ({fr} frames, "
                          f"{dt:.1f} s wall, {threads} worker threads): oracle fbank+CMVN (C) + TDNN-S with "
                          f"single-threaded OpenBLAS sgemm per worker"}
 

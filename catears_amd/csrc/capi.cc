@@ -374,6 +374,7 @@ static int default_gemm() {
     if (e && !strcmp(e, "bf16x6")) return (int)CE_GPU_GEMM_BF16X6;
     if (e && !strcmp(e, "f16x3")) return (int)CE_GPU_GEMM_F16X3;
     if (e && !strcmp(e, "bf16x6p")) return (int)CE_GPU_GEMM_BF16X6_PLANES;
+    if (e && *e) return -1;  // unknown mode: model loads fail (CE_GPU_EINVAL)
     return (int)CE_GPU_GEMM_BF16X6;
   }();
   return g;
@@ -516,6 +517,9 @@ static int build_program(const std::vector<RawLayer> &layers, int left, int righ
   }
   m->x3_ok = m->x3_ok && m->x6_ok;
   const int want = default_gemm();
+  if (want < 0)
+    return fail(CE_GPU_EINVAL, std::string("CATEARS_NNET_GEMM=") + getenv("CATEARS_NNET_GEMM") +
+                                   ": not one of fp32, bf16x6, bf16x6p, f16x3");
   m->gemm = want == CE_GPU_GEMM_F16X3 && m->x3_ok   ? CE_GPU_GEMM_F16X3
             : want == CE_GPU_GEMM_BF16X6_PLANES && m->x6_ok ? CE_GPU_GEMM_BF16X6_PLANES
             : want != CE_GPU_GEMM_FP32 && m->x6_ok ? CE_GPU_GEMM_BF16X6
@@ -641,7 +645,7 @@ extern "C" {
 
 const char *ce_gpu_last_error(void) { return g_last_error.c_str(); }
 
-const char *ce_gpu_version(void) { return "catears-mi355x 0.1 (gfx950)"; }
+const char *ce_gpu_version(void) { return "catears-mi355x 0.3 (gfx950)"; }
 
 int ce_gpu_ctx_create(int device, void *stream, ce_gpu_ctx **out) {
   if (!out) return fail(CE_GPU_EINVAL, "out is NULL");
@@ -984,6 +988,12 @@ int ce_gpu_fbank(ce_gpu_ctx *ctx, const ce_gpu_plan *p, const float *d_pcm, floa
   return launch_fbank(ctx->stream, ctx->d_tables.as<FbankTables>(), p, d_pcm, d_feats, d_mel);
 }
 
+int ce_gpu_fbank_s16(ce_gpu_ctx *ctx, const ce_gpu_plan *p, const int16_t *d_pcm, float *d_feats, float *d_mel) {
+  if (!ctx || !p || (p->total_frames > 0 && (!d_pcm || !d_feats))) return fail(CE_GPU_EINVAL, "NULL argument");
+  ProfScope prof(ctx, CE_GPU_PROF_FBANK);
+  return launch_fbank_s16(ctx->stream, ctx->d_tables.as<FbankTables>(), p, d_pcm, d_feats, d_mel);
+}
+
 int ce_gpu_cmvn(ce_gpu_ctx *ctx, const ce_gpu_plan *p, const float *d_global_stats, const float *d_feats,
                 float *d_out) {
   if (!ctx || !p || !d_global_stats || (p->total_frames > 0 && (!d_feats || !d_out)))
@@ -1107,9 +1117,16 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
   // rule for measurements)
   static const int *rule = [] {
     static int r[3] = {6, 8, 64};
-    if (const char *e = getenv("CATEARS_LAT_SLICES")) sscanf(e, "%d,%d,%d", &r[0], &r[1], &r[2]);
+    if (const char *e = getenv("CATEARS_LAT_SLICES")) {
+      int v[3];
+      if (sscanf(e, "%d,%d,%d", &v[0], &v[1], &v[2]) != 3 || v[0] < 1 || v[1] < 1 || v[2] < 1) return (int *)nullptr;
+      r[0] = v[0], r[1] = v[1], r[2] = v[2];
+    }
     return r;
   }();
+  if (ctx->latency && !rule)
+    return fail(CE_GPU_EINVAL, std::string("CATEARS_LAT_SLICES=") + getenv("CATEARS_LAT_SLICES") +
+                                   ": expected three positive integers min_ktiles,max_slices,target_blocks");
   auto slices = [](int kpad, int n) {
     const int cols = (n + 127) / 128, kt = kpad / 32;
     const int s = std::max(1, std::min(std::min(rule[1], kt / rule[0]), (rule[2] + cols - 1) / cols));
@@ -1588,11 +1605,8 @@ int ce_gpu_nnet_propagate_blocks(ce_gpu_ctx *ctx, const ce_gpu_model *m, const f
                          subtract_prior ? m->log_prior.as<float>() : nullptr, d_dst, d_out);
 }
 
-int ce_gpu_score(ce_gpu_ctx *ctx, const ce_gpu_model *m, const ce_gpu_plan *p, const float *d_pcm,
-                 const float *d_global_stats, float *d_feats_ws, float *d_loglik) {
-  if (!ctx || !m || !p) return fail(CE_GPU_EINVAL, "NULL argument");
-  if (m->input_dim != kMel) return fail(CE_GPU_EINVAL, "nnet input is not 40-dim fbank");
-  CE_TRY(ce_gpu_fbank(ctx, p, d_pcm, d_feats_ws, nullptr));
+static int score_feats(ce_gpu_ctx *ctx, const ce_gpu_model *m, const ce_gpu_plan *p, const float *d_global_stats,
+                       float *d_feats_ws, float *d_loglik) {
   const float *feats = d_feats_ws;
   if (d_global_stats) {
     float *norm = d_feats_ws + (size_t)p->total_frames * kMel;
@@ -1600,6 +1614,22 @@ int ce_gpu_score(ce_gpu_ctx *ctx, const ce_gpu_model *m, const ce_gpu_plan *p, c
     feats = norm;
   }
   return ce_gpu_am_forward(ctx, m, p, feats, d_loglik);
+}
+
+int ce_gpu_score(ce_gpu_ctx *ctx, const ce_gpu_model *m, const ce_gpu_plan *p, const float *d_pcm,
+                 const float *d_global_stats, float *d_feats_ws, float *d_loglik) {
+  if (!ctx || !m || !p) return fail(CE_GPU_EINVAL, "NULL argument");
+  if (m->input_dim != kMel) return fail(CE_GPU_EINVAL, "nnet input is not 40-dim fbank");
+  CE_TRY(ce_gpu_fbank(ctx, p, d_pcm, d_feats_ws, nullptr));
+  return score_feats(ctx, m, p, d_global_stats, d_feats_ws, d_loglik);
+}
+
+int ce_gpu_score_s16(ce_gpu_ctx *ctx, const ce_gpu_model *m, const ce_gpu_plan *p, const int16_t *d_pcm,
+                     const float *d_global_stats, float *d_feats_ws, float *d_loglik) {
+  if (!ctx || !m || !p) return fail(CE_GPU_EINVAL, "NULL argument");
+  if (m->input_dim != kMel) return fail(CE_GPU_EINVAL, "nnet input is not 40-dim fbank");
+  CE_TRY(ce_gpu_fbank_s16(ctx, p, d_pcm, d_feats_ws, nullptr));
+  return score_feats(ctx, m, p, d_global_stats, d_feats_ws, d_loglik);
 }
 
 int ce_gpu_sgemm(ce_gpu_ctx *ctx, int m, int n, int k, const float *d_a, int lda, const float *d_b, int ldb,

@@ -312,6 +312,8 @@ namespace catears {
 // Kernel launchers (kernels/*.hip).  All enqueue on `s` and return a status.
 int launch_fbank(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, const float *pcm,
                  float *feats, float *mel);
+int launch_fbank_s16(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, const int16_t *pcm,
+                     float *feats, float *mel);
 int launch_cmvn(hipStream_t s, const ce_gpu_plan *p, const float *gstats, const float *in,
                 float *out);
 

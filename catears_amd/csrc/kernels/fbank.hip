@@ -71,8 +71,13 @@ struct BlockTables {
 // only global traffic is the 1.6 kB PCM read and the 160 B feature write.
 // 5 waves per SIMD (the LDS bound; unrolled, the compiler would otherwise
 // take 117 VGPRs and 4 waves)
+// Sample: float (raw int16 scale, the Vector<float> WaveReader::Process
+// produces) or int16_t (the WAV payload itself, converted here exactly as
+// src/pcm_reader.cc:174 does on the host -- int16 -> float is exact, so both
+// inputs give the same bits; 2 B per sample read instead of 4).
+template <typename Sample>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) void fbank_kernel(const FbankTables *__restrict__ tab,
-                                                    const float *__restrict__ pcm,
+                                                    const Sample *__restrict__ pcm,
                                                     const int64_t *__restrict__ sample_off,
                                                     const int64_t *__restrict__ frame_off,
                                                     const int *__restrict__ block_utt,
@@ -113,7 +118,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
   for (int64_t f = (int64_t)blockIdx.x * kFramesPerBlock + wave; f < total_frames; f += stride) {
     int u = block_utt[f / kFramesPerBlock];
     while (f >= frame_off[u + 1]) ++u;
-    const float *src = pcm + sample_off[u] + (f - frame_off[u]) * kShift;
+    const Sample *src = pcm + sample_off[u] + (f - frame_off[u]) * kShift;
 
     // 1. samples + DC offset (sum exact for integer-valued PCM: any order)
     float v[7];
@@ -121,7 +126,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
 #pragma unroll
     for (int j = 0; j < 7; ++j) {
       const int i = lane + 64 * j;
-      v[j] = i < kWinLen ? src[i] : 0.0f;
+      v[j] = i < kWinLen ? (float)src[i] : 0.0f;
       part += v[j];
     }
     const float mean = wave_sum(part) / (float)kWinLen;
@@ -178,18 +183,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) voi
   }
 }
 
-}  // namespace
-
-int launch_fbank(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, const float *pcm,
-                 float *feats, float *mel) {
+template <typename Sample>
+int launch_fbank_t(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, const Sample *pcm, float *feats,
+                   float *mel) {
   if (p->total_frames == 0) return CE_GPU_OK;
   const int64_t blocks = (p->total_frames + kFramesPerBlock - 1) / kFramesPerBlock;
   const unsigned grid = (unsigned)(blocks < kMaxBlocks ? blocks : kMaxBlocks);
-  hipLaunchKernelGGL(fbank_kernel, dim3(grid), dim3(256), 0, s, d_tab, pcm,
+  hipLaunchKernelGGL(fbank_kernel<Sample>, dim3(grid), dim3(256), 0, s, d_tab, pcm,
                      p->d_sample_off.as<int64_t>(), p->d_frame_off.as<int64_t>(),
                      p->d_block_utt.as<int>(), p->total_frames, feats, mel);
   CE_HIP(hipGetLastError());
   return CE_GPU_OK;
+}
+
+}  // namespace
+
+int launch_fbank(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, const float *pcm,
+                 float *feats, float *mel) {
+  return launch_fbank_t(s, d_tab, p, pcm, feats, mel);
+}
+
+int launch_fbank_s16(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, const int16_t *pcm,
+                     float *feats, float *mel) {
+  return launch_fbank_t(s, d_tab, p, pcm, feats, mel);
 }
 
 int fbank_frames_per_block() { return kFramesPerBlock; }

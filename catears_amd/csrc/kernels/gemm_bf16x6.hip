@@ -353,7 +353,7 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6q_kernel(X6Args p) {
 // SCHED: 0 = split of tile kt+1 before the MFMAs of tile kt (round 1);
 // 6 = MFMAs first; 8 = MFMAs first in explicit regions (the default).
 // DIAG (ablation builds of the SCHED 6 loop, wrong results; timing only,
-// DESIGN.md §8): bit 1 = no split (raw fp32 bits as the three planes),
+// DESIGN.md §8; compiled only with -DCATEARS_DIAG, `make EXPERIMENTS=1`): bit 1 = no split (raw fp32 bits as the three planes),
 // 2 = no global loads after the prologue, 4 = no MFMAs, 8 = no fragment
 // reads after the first tile, 16 = no K-tile barrier, 32 = no plane writes
 // after the prologue.
@@ -363,6 +363,9 @@ template <class C, int SCHED, int DIAG = 0, bool SPLIT = false>
 __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
   constexpr int BW = C::BW, BF = C::BF, TW = C::TW, TF = C::TF, NT = C::NT, STAGE = C::STAGE;
   static_assert(!SPLIT || SCHED == 0, "split-K runs in the SCHED 0 loop");
+#ifndef CATEARS_DIAG
+  static_assert(DIAG == 0, "ablation builds (wrong results) only with -DCATEARS_DIAG");
+#endif
   constexpr int RPP = NT / 4;  // rows per pass (4 threads x 32 B per row)
   static_assert(BW % RPP == 0 && BF % RPP == 0, "rows per pass");
   constexpr int NPW = BW / RPP, NPX = BF / RPP;
@@ -653,8 +656,8 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
     // add returns S-1 reads the other slices' partials with 8-B agent-scope
     // loads and sums all S in slice order -- the same value whichever slice
     // arrives last -- and runs the epilogue; the others exit.  No release
-    // fence (it would write back the XCD's dirty L2) and no wave ever waits
-    // on another block.
+    // fence (it would write back the XCD's dirty L2); the winner acquires.
+    // No wave ever waits on another block.
     constexpr int WF4 = TW * TF * 64;  // f32x4 per wave and slice
     typedef unsigned long long u64;
     u64 *base = reinterpret_cast<u64 *>(p.part) + 2 * ((size_t)tile * p.splitk * C::NW * WF4 + wave * WF4 + lane);
@@ -671,8 +674,25 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __shared__ unsigned s_arrived;
     __syncthreads();
-    if (tid == 0)
+    if (tid == 0) {
       s_arrived = __hip_atomic_fetch_add(p.ticket + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // The last arriver acquires at agent scope before any wave of its
+      // block reads the other slices' partials (buffer_inv sc1 of this CU's
+      // L1, then the wait for it, then the barrier that releases the other
+      // waves).  The partial loads below are sc1 besides, so the hand-off is
+      // ordered by the language's acquire and not only by the ISA's L1
+      // bypass.  The store side needs no release fence: each slice's partials
+      // are sc1 (write-through) stores, drained by every storing wave's
+      // vmcnt(0) before the block barrier that precedes the ticket add --
+      // they have left this XCD's L2 before the add can be seen
+      // (MI355X_MICROARCH.md, hand-off table, first row).  A release here
+      // would write back the XCD's whole dirty L2 per block (the 30 % loss
+      // DESIGN.md §8 records).
+      if (s_arrived == (unsigned)p.splitk - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
     __syncthreads();
     if (s_arrived != (unsigned)p.splitk - 1) return;
     if (tid == 0) __hip_atomic_store(p.ticket + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
@@ -944,6 +964,14 @@ typedef X6Cfg<128, 64, 2, 2, 2> X6LatSmallCfg;
 constexpr int kX6LatSmallRows = 256;
 constexpr int kX6LatSmallPad = 82 * 1024 - 2 * X6LatSmallCfg::STAGE;
 
+// CATEARS_X6_VARIANT: the schedule of the default (fp32-operand) kernel.
+// The product build carries the default (0 = 160, region-scheduled 128 x 256
+// tiles) and the two documented deployment alternatives, all bit-identical
+// (tests/test_gpu_x6_variants.py): 40 (128 x 128 tiles, one batch at a time
+// on an idle GPU) and 200 (warp-specialised 128 x 128).  Measurement
+// variants -- and the DIAG ablations, which give wrong results -- exist only
+// in `make EXPERIMENTS=1` builds (libcatears_hip_exp.so, tools/); any other
+// value makes every bf16x6 launch fail with CE_GPU_EINVAL.
 int x6_variant() {
   static int v = [] {
     const char *e = getenv("CATEARS_X6_VARIANT");
@@ -1016,18 +1044,24 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
                                   : launch_f_split<X6LatCfg>(s, p, a);
   if (f32in) {
     switch (x6_variant()) {
+      case 0:
+      case 160:  // region-scheduled loop (the default)
+        return launch_f<X6Cfg<128, 256, 2, 4, 2>, 8>(s, p);
       case 40:  // 128 x 128 tiles: fills all CUs on a 1024-wide layer (one batch at a time on an idle GPU)
         return launch_f<X6Cfg<128, 128, 4, 2, 2>>(s, p);
+      case 200:  // warp-specialised: 4 MFMA waves (64 x 64 each) + 4 producer waves
+        return launch_ws<X6Cfg<128, 128, 2, 2, 2>, 4>(s, p);
+#ifdef CATEARS_EXPERIMENTS
       case 42:  // round-1 default: split of tile kt+1, then the MFMAs of tile kt
         return launch_f<X6Cfg<128, 256, 2, 4, 2>>(s, p);
       case 55:  // MFMAs of tile kt first, the split interleaved by the compiler
         return launch_f<X6Cfg<128, 256, 2, 4, 2>, 6>(s, p);
-      case 200:  // warp-specialised: 4 MFMA waves (64 x 64 each) + 4 producer waves
-        return launch_ws<X6Cfg<128, 128, 2, 2, 2>, 4>(s, p);
       case 202:  // 128 x 256: 4 MFMA waves of 64 x 128 + 4 producers
         return launch_ws<X6Cfg<128, 256, 2, 2, 2>, 4>(s, p);
       case 204:  // 128 x 256: 8 MFMA waves of 64 x 64 + 4 producers (3 waves per SIMD)
         return launch_ws<X6Cfg<128, 256, 2, 4, 2>, 4>(s, p);
+#endif
+#ifdef CATEARS_DIAG
       // ablations of 55 (wrong results: timing only)
       case 91:
         return launch_f<X6Cfg<128, 256, 2, 4, 2>, 6, 1>(s, p);
@@ -1049,8 +1083,11 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
         return launch_f<X6Cfg<128, 256, 2, 4, 2>, 6, 32>(s, p);
       case 103:
         return launch_f<X6Cfg<128, 256, 2, 4, 2>, 6, 43>(s, p);
-      default:  // = 160: region-scheduled loop
-        return launch_f<X6Cfg<128, 256, 2, 4, 2>, 8>(s, p);
+#endif
+      default:
+        return fail(CE_GPU_EINVAL, "CATEARS_X6_VARIANT=" + std::to_string(x6_variant()) +
+                                       " is not a schedule of this build (product: 0, 40, 200; others need "
+                                       "`make EXPERIMENTS=1`)");
     }
   }
   // plane operands (CATEARS_X6_F32IN=0 / CE_GPU_GEMM_BF16X6_PLANES)

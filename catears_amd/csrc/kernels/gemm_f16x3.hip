@@ -353,6 +353,10 @@ int launch_gemm_f16x3(hipStream_t s, const X3Gemm &a) {
   // K-tiles of 64 need every segment (and the padded K) a multiple of 64
   const bool k64 = a.din % 64 == 0 && a.kpad % 64 == 0;
   switch (x3_variant()) {
+    case 0:
+      return k64 ? launch_cfg<X3Cfg<128, 128, 2, 4, 2, 64>>(s, p, out16)
+                 : launch_cfg<X3Cfg<128, 128, 2, 4, 3, 32>>(s, p, out16);
+#ifdef CATEARS_EXPERIMENTS
     case 1:
       return launch_cfg<X3Cfg<128, 128, 2, 4, 3, 32>>(s, p, out16);
     case 2:
@@ -369,9 +373,10 @@ int launch_gemm_f16x3(hipStream_t s, const X3Gemm &a) {
     case 7:
       return k64 ? launch_cfg<X3Cfg<64, 256, 1, 4, 2, 64>>(s, p, out16)
                  : launch_cfg<X3Cfg<128, 256, 2, 4, 3, 32>>(s, p, out16);
+#endif
     default:
-      return k64 ? launch_cfg<X3Cfg<128, 128, 2, 4, 2, 64>>(s, p, out16)
-                 : launch_cfg<X3Cfg<128, 128, 2, 4, 3, 32>>(s, p, out16);
+      return fail(CE_GPU_EINVAL, "CATEARS_X3_VARIANT=" + std::to_string(x3_variant()) +
+                                     " is not a kernel of this build (product: 0; others need `make EXPERIMENTS=1`)");
   }
 }
 

@@ -697,7 +697,8 @@ int launch_glds(hipStream_t s, KArgs p, bool a_fast, bool b_nmajor, bool rm) {
 // nnet streams (tools/gemm_variants.sh: 115.5 TF vs 110.5 for the register-
 // staged 64 x 128 pipeline).  Layers it cannot take (the first layer's
 // gather, N-major MatMat operands) fall back to pipe2 64 x 128.
-// CATEARS_GEMM_VARIANT overrides for tuning.
+// CATEARS_GEMM_VARIANT selects another tiling in `make EXPERIMENTS=1` builds
+// (tools/); a value this build does not carry fails with CE_GPU_EINVAL.
 constexpr int kDefaultVariant = 29;
 
 int variant() {
@@ -760,8 +761,11 @@ int launch_gemm_f32(hipStream_t s, const GemmArgs &a) {
   if (a_fast && (int64_t)(a.row_map ? INT32_MAX / 4 : a.m) * a.ldx * 4 >= (int64_t)1 << 32 && !a.row_map)
     return fail(CE_GPU_EINVAL, "gemm_f32: activation block beyond 4 GiB");
   // K-tiles deeper than 32 only where K allows it
-  const bool deep = a.kpad % 64 == 0;
+  [[maybe_unused]] const bool deep = a.kpad % 64 == 0;
   switch (variant()) {
+    case kDefaultVariant:
+      return launch_glds<V2, 2>(s, p, a_fast, a.b_nmajor, rm);
+#ifdef CATEARS_EXPERIMENTS  // tools/gemm_variants.sh
     case 1:
       return deep ? launch_cfg<V1>(s, p, a_fast, a.b_nmajor, rm) : launch_cfg<V0>(s, p, a_fast, a.b_nmajor, rm);
     case 2:
@@ -812,8 +816,6 @@ int launch_gemm_f32(hipStream_t s, const GemmArgs &a) {
       return deep ? launch_glds<W3, 2>(s, p, a_fast, a.b_nmajor, rm) : launch_glds<W0>(s, p, a_fast, a.b_nmajor, rm);
     case 28:
       return launch_glds<W0, 2>(s, p, a_fast, a.b_nmajor, rm);
-    case 29:
-      return launch_glds<V2, 2>(s, p, a_fast, a.b_nmajor, rm);
     case 30:
       return launch_glds<V8, 2>(s, p, a_fast, a.b_nmajor, rm);
     case 31:
@@ -830,8 +832,10 @@ int launch_gemm_f32(hipStream_t s, const GemmArgs &a) {
       return launch_glds<V2, 3, true>(s, p, a_fast, a.b_nmajor, rm);
     case 35:
       return deep ? launch_glds<V1, 2>(s, p, a_fast, a.b_nmajor, rm) : launch_glds<V0, 2>(s, p, a_fast, a.b_nmajor, rm);
+#endif
     default:
-      return launch_cfg<V0>(s, p, a_fast, a.b_nmajor, rm);
+      return fail(CE_GPU_EINVAL, "CATEARS_GEMM_VARIANT=" + std::to_string(variant()) +
+                                     " is not a kernel of this build (product: 29; others need `make EXPERIMENTS=1`)");
   }
 }
 

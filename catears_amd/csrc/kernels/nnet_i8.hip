@@ -722,6 +722,13 @@ int launch_i8_gemm(hipStream_t s, const I8Layer &L, const int8_t *a, int lda, in
       hipLaunchKernelGGL(kern, dim3(p.tiles_m * p.tiles_n), dim3(threads), 0, s, p);
     };
     switch (use_glds) {
+      // 15: 256 x 128, 3 stages (144 KiB), 8 waves of 64 x 64: one tile per
+      // CU on the 1024-wide layers and two K-tiles in flight.  The serial
+      // per-layer times of 1, 7, 10, 11 and 15 are within 5 % of each other
+      // (the loop waits on L2 / MALL fetches, 43 % of wave cycles parked, MFMA
+      // busy ~20 %); 9 (128 tiles) leaves half the CUs idle when alone.
+      case 15: go(gemm_i8_glds_kernel<256, 128, 3, 4, 2>, 256, 128, 512); break;
+#ifdef CATEARS_EXPERIMENTS  // tools/i8_sweep.sh
       case 2: go(gemm_i8_glds_kernel<128, 128, 3>, 128, 128); break;
       case 3: go(gemm_i8_glds_kernel<128, 128, 4>, 128, 128); break;
       case 4: go(gemm_i8_glds_kernel<128, 64, 4>, 128, 64); break;
@@ -735,17 +742,16 @@ int launch_i8_gemm(hipStream_t s, const I8Layer &L, const int8_t *a, int lda, in
       case 9: go(gemm_i8_glds_kernel<256, 256, 2, 4, 2>, 256, 256, 512); break;
       case 10: go(gemm_i8_reg_kernel<128, 128, 2, 2>, 128, 128, 256); break;
       case 11: go(gemm_i8_reg_kernel<256, 128, 4, 2>, 256, 128, 512); break;
-      // 15: 256 x 128, 3 stages (144 KiB), 8 waves of 64 x 64: one tile per
-      // CU on the 1024-wide layers and two K-tiles in flight.  The serial
-      // per-layer times of 1, 7, 10, 11 and 15 are within 5 % of each other
-      // (the loop waits on L2 / MALL fetches, 43 % of wave cycles parked, MFMA
-      // busy ~20 %); 9 (128 tiles) leaves half the CUs idle when alone.
-      case 15: go(gemm_i8_glds_kernel<256, 128, 3, 4, 2>, 256, 128, 512); break;
       // 20-22: branch-free, DMA two K-tiles ahead (gemm_i8_q_kernel)
       case 20: go(gemm_i8_q_kernel<256, 128, 4, 2>, 256, 128, 512); break;
       case 21: go(gemm_i8_q_kernel<128, 256, 2, 4>, 128, 256, 512); break;
       case 22: go(gemm_i8_q_kernel<128, 128, 2, 2>, 128, 128, 256); break;
-      default: go(gemm_i8_glds_kernel<128, 128, 2>, 128, 128); break;
+      case 1: go(gemm_i8_glds_kernel<128, 128, 2>, 128, 128); break;
+#endif
+      default:
+        return fail(CE_GPU_EINVAL, "CATEARS_I8_GEMM=" + std::to_string(use_glds) +
+                                       " is not a kernel of this build (product: 15, or 0 for the register-staged "
+                                       "fallback; others need `make EXPERIMENTS=1`)");
     }
     CE_HIP(hipGetLastError());
     return CE_GPU_OK;

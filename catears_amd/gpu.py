@@ -31,6 +31,7 @@ ABI = [
     "ce_gpu_profile_anchor", "ce_gpu_ctx_profile_intervals", "ce_gpu_model_quantize",
     "ce_gpu_nnet_propagate_blocks", "ce_gpu_loglik_gather", "ce_gpu_loglik_columns",
     "ce_gpu_model_set_gemm", "ce_gpu_model_get_gemm", "ce_gpu_ctx_overflow", "ce_gpu_ctx_set_latency",
+    "ce_gpu_fbank_s16", "ce_gpu_score_s16",
 ]
 
 # ce_gpu_model_set_gemm modes
@@ -77,9 +78,11 @@ def lib():
         "ce_gpu_plan_frame_offsets": (ci, [vp, pi64]),
         "ce_gpu_plan_destroy": (ci, [vp]),
         "ce_gpu_fbank": (ci, [vp, vp, vp, vp, vp]),
+        "ce_gpu_fbank_s16": (ci, [vp, vp, vp, vp, vp]),
         "ce_gpu_cmvn": (ci, [vp, vp, vp, vp, vp]),
         "ce_gpu_am_forward": (ci, [vp, vp, vp, vp, vp]),
         "ce_gpu_score": (ci, [vp, vp, vp, vp, vp, vp, vp]),
+        "ce_gpu_score_s16": (ci, [vp, vp, vp, vp, vp, vp, vp]),
         "ce_gpu_sgemm": (ci, [vp, ci, ci, ci, vp, ci, vp, ci, vp, ci]),
         "ce_gpu_quantize": (ci, [vp, vp, i64, vp, vp]),
         "ce_gpu_gemm_u8u8f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp]),
@@ -313,10 +316,15 @@ class Plan:
 
 
 def fbank(ctx, plan, pcm, feats=None, mel=None):
+    """Fbank::Process over the plan's utterances; `pcm` is float32 at raw
+    int16 scale (ce_gpu_fbank) or int16 (ce_gpu_fbank_s16)."""
     import torch
     if feats is None:
         feats = torch.empty((plan.total_frames, 40), dtype=torch.float32, device=pcm.device)
-    check(lib().ce_gpu_fbank(ctx.h, plan.h, _ptr(pcm), _ptr(feats), _ptr(mel)))
+    fn = lib().ce_gpu_fbank_s16 if pcm.dtype == torch.int16 else lib().ce_gpu_fbank
+    if pcm.dtype not in (torch.int16, torch.float32):
+        raise TypeError("pcm must be float32 or int16")
+    check(fn(ctx.h, plan.h, _ptr(pcm), _ptr(feats), _ptr(mel)))
     return feats
 
 
@@ -342,7 +350,10 @@ def score(ctx, model, plan, pcm, global_stats=None, ws=None, out=None):
         ws = torch.empty((2 * plan.total_frames * 40 + 1,), dtype=torch.float32, device=pcm.device)
     if out is None:
         out = torch.empty((plan.total_frames, model.num_pdfs), dtype=torch.float32, device=pcm.device)
-    check(lib().ce_gpu_score(ctx.h, model.h, plan.h, _ptr(pcm), _ptr(global_stats), _ptr(ws), _ptr(out)))
+    if pcm.dtype not in (torch.int16, torch.float32):
+        raise TypeError("pcm must be float32 or int16")
+    fn = lib().ce_gpu_score_s16 if pcm.dtype == torch.int16 else lib().ce_gpu_score
+    check(fn(ctx.h, model.h, plan.h, _ptr(pcm), _ptr(global_stats), _ptr(ws), _ptr(out)))
     return out
 
 

@@ -67,6 +67,7 @@ class AcousticModel {
   int chunk_size_ = 0;
   int num_pdfs_ = 0;
   int feat_dim_ = 0;
+  int latency_ = 1;  // gpu_latency_mode: applied to the shared context per call
   Vector<int32_t> tid2pdf_;
   std::unique_ptr<Batcher> batcher_;
 

@@ -96,10 +96,10 @@ Status AcousticModel::Read(const Configuration &conf) {
   int pdfs = 0;
   ce_gpu_model_info(model_, nullptr, nullptr, &feat_dim_, &pdfs, nullptr, nullptr);
   // streaming chunks are small row blocks: latency mode (split-K GEMMs,
-  // ce_gpu_ctx_set_latency) unless the config turns it off; the process-wide
-  // context follows the last model loaded
-  if (ce_gpu_ctx_set_latency(rt.ctx(), conf.GetIntegerOrElse("gpu_latency_mode", 1)) != CE_GPU_OK)
-    return Status::RuntimeError(util::Format("gpu_latency_mode: {}", ce_gpu_last_error()));
+  // ce_gpu_ctx_set_latency) unless the config turns it off.  The flag is this
+  // model's: RunBlocks sets it on the shared context for each of its calls,
+  // so models loaded later with another setting do not change it.
+  latency_ = conf.GetIntegerOrElse("gpu_latency_mode", 1) ? 1 : 0;
   batcher_.reset(new Batcher());
   batcher_->max_blocks = conf.GetIntegerOrElse("gpu_batch_streams", 1);
   batcher_->wait = std::chrono::microseconds(conf.GetIntegerOrElse("gpu_batch_wait_us", 200));
@@ -196,6 +196,7 @@ void AcousticModel::RunBlocks(const std::vector<const float *> &rows, const std:
     rt.Upload(d_in + at * dim, dim, rows[b], dim, sizeof(float), n[b], dim);
     at += n[b];
   }
+  Check(ce_gpu_ctx_set_latency(rt.ctx(), latency_), "AcousticModel::ComputeBatch");
   if (rows.size() == 1)
     Check(ce_gpu_nnet_propagate(rt.ctx(), model_, d_in, n[0], dim, 1, d_out), "AcousticModel::ComputeBatch");
   else

@@ -1,24 +1,56 @@
-"""Utterance sharding and the log-likelihood gather.
+"""Utterance sharding, the C4 corpus and the log-likelihood gather.
 
 Utterances are independent through fbank, CMVN (per-utterance window +
-constant global stats) and the TDNN (context never crosses utterances), so a
-node shards them across GPUs with no data-path collective.  The only exchange
-is the north star's: every rank's log-likelihood batches are gathered to
-rank 0 (RCCL over xGMI when the backend is "nccl"), streamed per batch into
-a small ring of receive buffers -- 100 h of TDNN-S posteriors are ~497 GB,
-more than one GPU's 288 GB, so rank 0 consumes (here: checksums) each batch
-instead of storing the run.
+constant global stats) and the TDNN (context never crosses utterances): the
+reference keeps every per-utterance state in its own Instance objects
+(src/ce_stt.cc:53-60) and the AM's output does not depend on how its rows are
+chunked (src/am.cc:73-80,115-164).  A node therefore shards utterances across
+GPUs with no data-path collective.  The one exchange is the north star's:
+every rank's log-likelihood batches go to rank 0 (RCCL point-to-point over
+xGMI when the backend is "nccl"), streamed per batch into a small ring of
+receive buffers -- 100 h of TDNN-S posteriors are ~497 GB, more than one GPU's
+288 GB, so rank 0 consumes (here: checksums every row of) each batch instead
+of storing the run.
 
-Backend-agnostic: the same code runs on CPU tensors with gloo (tests).
+Backend-agnostic: the same code runs on CPU tensors with gloo (tests), and
+stages CUDA tensors through the host when the backend is gloo (one-GPU
+rehearsals of N ranks).
 """
+import numpy as np
 import torch
 import torch.distributed as dist
+
+FRAME_LEN, FRAME_SHIFT = 400, 160   # src/fbank.h:7-13
+C4_UTTS = 36000                     # 100 h of 10 s-average utterances
+C4_PAIR_SAMPLES = 320000            # two utterances per 20 s pair
+C4_MIN_SAMPLES = 32000              # 2 s
+
+
+def num_frames(n):
+    """Fbank frames of n samples (src/fbank.cc:35-42)."""
+    return 0 if n < FRAME_LEN else 1 + (n - FRAME_LEN) // FRAME_SHIFT
+
+
+def c4_corpus(n_utts=C4_UTTS, seed=20250117):
+    """Sample counts of the C4 corpus: a seeded length mix of 2-18 s
+    utterances in pairs (a, 320000 - a) with a uniform over [2 s, 18 s], so
+    the corpus is exactly n_utts x 10 s of audio (100 h at the default
+    36 000 utterances) while no two neighbours need have the same length."""
+    from .synth import splitmix64
+    if n_utts % 2:
+        raise ValueError("the C4 corpus is built from pairs of utterances")
+    span = C4_PAIR_SAMPLES - 2 * C4_MIN_SAMPLES + 1
+    a = C4_MIN_SAMPLES + (splitmix64(seed, n_utts // 2) % np.uint64(span)).astype(np.int64)
+    out = np.empty(n_utts, np.int64)
+    out[0::2] = a
+    out[1::2] = C4_PAIR_SAMPLES - a
+    return out
 
 
 def shard_utterances(lengths, world, rank):
     """Longest-first greedy assignment by frame count: returns the indices of
-    the utterances rank `rank` scores (deterministic, balanced within one
-    utterance's length)."""
+    the utterances rank `rank` scores, ascending (deterministic, balanced
+    within one utterance's length)."""
     order = sorted(range(len(lengths)), key=lambda i: (-int(lengths[i]), i))
     load = [0] * world
     owner = [0] * len(lengths)
@@ -29,63 +61,148 @@ def shard_utterances(lengths, world, rank):
     return [i for i in range(len(lengths)) if owner[i] == rank]
 
 
-class LoglikGather:
-    """Asynchronous gather of equally shaped per-step batches to rank 0.
+def pack_batches(frames, left, right, max_rows=4096):
+    """Consecutive utterances into frame batches of at most `max_rows` packed
+    rows (T + L + R per utterance, the layout ce_gpu_plan_create packs):
+    returns lists of positions into `frames`.  An utterance longer than a
+    batch gets a batch of its own (the plan then splits it into overlapping
+    chunks, src/am.cc:73-80)."""
+    batches, cur, rows = [], [], 0
+    for i, t in enumerate(frames):
+        if t <= 0:
+            continue  # no frames, no rows (fbank returns 0 x 40)
+        need = int(t) + left + right
+        if cur and rows + need > max_rows:
+            batches.append(cur)
+            cur, rows = [], 0
+        cur.append(i)
+        rows += need
+    if cur:
+        batches.append(cur)
+    return batches
 
-    submit(t) launches the gather of `t` (a tensor this rank must not modify
-    until the returned slot is recycled, `depth` submits later); rank 0 gets
-    the world's batches in a ring of `depth` receive sets.  Rank 0 stands in
-    for the decoder that would consume them by folding the first row of each
-    received batch into a float64 checksum (proof of arrival, without adding
-    a full extra pass over every batch to rank 0's HBM traffic).
+
+class RowGather:
+    """Streams every rank's variable-length row batches to rank 0.
+
+    `counts[r][s]` is the number of rows rank r contributes at step s (0 or
+    absent: none), known to every rank from a setup exchange
+    (exchange_counts).  submit(s, t) sends this rank's rows of step s (rank
+    0: posts the receives of every peer's step-s rows into ring slot s %
+    depth, grouped into one batch_isend_irecv, and folds every received row
+    -- and, with own=, its own rows -- into a float64 checksum: the stand-in
+    for the decoder that would consume them).  A sender must not modify `t`
+    until wait_slot(s % depth) returns.  CUDA tensors go through RCCL on the
+    "nccl" backend; on gloo they are staged through host memory.
     """
 
-    def __init__(self, shape, dtype, device, depth=3, group=None):
+    def __init__(self, counts, width, dtype, device, depth=3, group=None, keep=False):
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.group = group
+        self.counts = [list(c) for c in counts]
+        self.width = width
         self.depth = depth
-        self.pending = [None] * depth
+        self.device = torch.device(device)
+        self.staged = dist.get_backend(group) == "gloo" and self.device.type == "cuda"
+        self.pending = [None] * depth  # (works, retire callback) per slot
         self.recv = None
         if self.rank == 0:
-            self.recv = [[torch.empty(shape, dtype=dtype, device=device) for _ in range(self.world)]
+            rows = [max(c) if c else 0 for c in self.counts]
+            rdev = "cpu" if self.staged else self.device
+            self.recv = [[torch.empty((max(rows[p], 1), width), dtype=dtype, device=rdev) for p in range(self.world)]
                          for _ in range(depth)]
-        # one accumulator per slot: a slot's retirements are ordered through
-        # its gathers even when callers retire slots from different streams
-        self.sums = [torch.zeros((), dtype=torch.float64, device=device) for _ in range(depth)]
-        self.batches = 0
-        self.slot = 0
+        self.sums = [torch.zeros((), dtype=torch.float64, device=self.device) for _ in range(depth)]
+        self.rows_in = 0       # rows rank 0 received
+        self.batches = 0       # steps retired
+        self.keep = [] if keep else None  # (peer, step, host rows) -- tests only
 
-    def _retire(self, s):
-        w = self.pending[s]
-        if w is None:
+    def rows(self, r, s):
+        c = self.counts[r]
+        return c[s] if s < len(c) else 0
+
+    def _retire(self, slot):
+        pend = self.pending[slot]
+        if pend is None:
             return
-        w.wait()
-        self.pending[s] = None
-        if self.rank == 0:
-            for t in self.recv[s]:
-                self.sums[s] += t[0].double().sum()
+        works, after, stream = pend
+        self.pending[slot] = None
+        if stream is None:  # CPU tensors
+            for w in works:
+                w.wait()
+            if after is not None:
+                after()
+        else:
+            # the transfers and rank 0's checksums run on the stream the step
+            # was submitted from; the caller's stream then waits for all of
+            # it (its buffer may be overwritten after this returns)
+            with torch.cuda.stream(stream):
+                for w in works:
+                    w.wait()
+                if after is not None:
+                    after()
+                ev = torch.cuda.Event()
+                ev.record(stream)
+            torch.cuda.current_stream(self.device).wait_event(ev)
         self.batches += 1
 
-    def submit(self, t):
-        s = self.slot
-        self._retire(s)
-        self.pending[s] = dist.gather(t, self.recv[s] if self.rank == 0 else None, dst=0,
-                                      group=self.group, async_op=True)
-        self.slot = (s + 1) % self.depth
-        return s
+    def submit(self, s, t=None, own=None):
+        slot = s % self.depth
+        self._retire(slot)
+        ops, after = [], None
+        if self.rank != 0:
+            n = self.rows(self.rank, s)
+            if n:
+                assert t is not None and t.shape[0] >= n and t.shape[1] == self.width
+                src = t[:n]
+                if self.staged:
+                    src = src.cpu()
+                ops.append(dist.P2POp(dist.isend, src.contiguous(), 0, self.group))
+        else:
+            bufs = []
+            for p in range(1, self.world):
+                n = self.rows(p, s)
+                if n:
+                    b = self.recv[slot][p][:n]
+                    bufs.append((p, b))
+                    ops.append(dist.P2POp(dist.irecv, b, p, self.group))
+            acc = self.sums[slot]
+
+            def after():
+                for p, b in bufs:
+                    x = b.to(self.device, non_blocking=False) if self.staged else b
+                    acc.add_(torch.sum(x, dtype=torch.float64))
+                    self.rows_in += b.shape[0]
+                    if self.keep is not None:
+                        self.keep.append((p, s, b.cpu().numpy().copy()))
+            if own is not None:
+                acc.add_(torch.sum(own, dtype=torch.float64))
+        works = dist.batch_isend_irecv(ops) if ops else []
+        stream = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
+        self.pending[slot] = (works, after, stream)
+        return slot
+
+    def wait_slot(self, slot):
+        """Order the current stream (NCCL) or the host (gloo) after the
+        transfer occupying `slot`; after it that step's input may be
+        overwritten and (rank 0) its rows have been consumed."""
+        self._retire(slot)
+
+    def drain(self):
+        for i in range(self.depth):
+            self._retire(i)
+        return self.checksum
 
     @property
     def checksum(self):
         return sum(self.sums[1:], self.sums[0].clone())
 
-    def wait_slot(self, s):
-        """Order the current stream after the gather occupying slot s (NCCL:
-        a stream wait; gloo: the host blocks) -- after it, that gather's
-        input may be overwritten."""
-        self._retire(s)
 
-    def drain(self):
-        for s in range(self.depth):
-            self._retire((self.slot + s) % self.depth)
-        return self.checksum
+def exchange_counts(mine, group=None):
+    """Every rank's per-step row counts (and any other picklable per-step
+    description, e.g. utterance ids), gathered once at setup so rank 0 can
+    post exact-size receives."""
+    world = dist.get_world_size(group)
+    out = [None] * world
+    dist.all_gather_object(out, mine, group=group)
+    return out

@@ -56,7 +56,10 @@ typedef struct ce_gpu_plan ce_gpu_plan;   /* geometry of one batch of utterances
 /* Message of the last failure on this thread ("" if none). */
 const char *ce_gpu_last_error(void);
 
-/* Library version string. */
+/* Library version string, "catears-mi355x <abi> (gfx950)".  ABI history
+ * (INTEGRATION.md §5): 0.1 round 1; 0.2 ce_gpu_loglik_gather gained `dim`
+ * (argument 5) -- a caller built against 0.1 must be rebuilt; 0.3 adds the
+ * int16 PCM entry points (ce_gpu_fbank_s16, ce_gpu_score_s16). */
 const char *ce_gpu_version(void);
 
 /* ------------------------------------------------------------ context --- */
@@ -70,7 +73,10 @@ int ce_gpu_ctx_create(int device, void *stream, ce_gpu_ctx **out);
 int ce_gpu_ctx_destroy(ce_gpu_ctx *ctx);
 /* Later calls enqueue on `stream`.  The switch is ordered: `stream` waits
  * (device-side, no host block) for everything already queued on the old
- * stream, which may still be using the context's workspaces. */
+ * stream, which may still be using the context's workspaces -- so the old
+ * stream must still be alive when this is called (switch first, destroy the
+ * old stream afterwards; destroying a stream the context still uses is
+ * undefined, as for any HIP call on a destroyed stream). */
 int ce_gpu_ctx_set_stream(ce_gpu_ctx *ctx, void *stream);
 /* Block the host until all work enqueued through ctx has finished. */
 int ce_gpu_ctx_synchronize(ce_gpu_ctx *ctx);
@@ -239,6 +245,15 @@ int ce_gpu_plan_destroy(ce_gpu_plan *p);
 int ce_gpu_fbank(ce_gpu_ctx *ctx, const ce_gpu_plan *p, const float *d_pcm, float *d_feats,
                  float *d_mel);
 
+/* The same from 16-bit PCM as it sits in a WAV payload (little-endian int16,
+ * utterances back to back at the plan's sample offsets): the int16 -> float
+ * conversion WaveReader::Process does on the host (src/pcm_reader.cc:148-190,
+ * :174) happens in the kernel's loads, exactly, so the features are
+ * bit-identical to ce_gpu_fbank on the converted floats -- at 2 B per sample
+ * of HBM (and PCIe) traffic instead of 4. */
+int ce_gpu_fbank_s16(ce_gpu_ctx *ctx, const ce_gpu_plan *p, const int16_t *d_pcm, float *d_feats,
+                     float *d_mel);
+
 /* Online CMVN (src/cmvn.cc:35-110) over every utterance: d_global_stats is
  * the 41-float VEC0 payload (40 sums + count); frames are processed in order
  * per utterance exactly like GetFrame(0), GetFrame(1), ...  d_out must not
@@ -279,6 +294,10 @@ int ce_gpu_nnet_propagate_blocks(ce_gpu_ctx *ctx, const ce_gpu_model *m, const f
 int ce_gpu_score(ce_gpu_ctx *ctx, const ce_gpu_model *m, const ce_gpu_plan *p,
                  const float *d_pcm, const float *d_global_stats, float *d_feats_ws,
                  float *d_loglik);
+
+/* ce_gpu_score from 16-bit PCM (ce_gpu_fbank_s16 as its first stage). */
+int ce_gpu_score_s16(ce_gpu_ctx *ctx, const ce_gpu_model *m, const ce_gpu_plan *p, const int16_t *d_pcm,
+                     const float *d_global_stats, float *d_feats_ws, float *d_loglik);
 
 /* ------------------------------------------------------- linear algebra --- */
 

@@ -1,14 +1,17 @@
-"""Multi-rank logic of the benchmark on CPU (gloo, world size 2): utterance
-sharding and the streamed log-likelihood gather to rank 0."""
+"""Multi-rank logic of the benchmark on CPU (gloo, world size 2): the C4
+corpus, utterance sharding, batch packing and the streamed variable-length
+log-likelihood gather to rank 0."""
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from catears_amd.shard import LoglikGather, shard_utterances
+from catears_amd.shard import (C4_UTTS, RowGather, c4_corpus, exchange_counts, num_frames, pack_batches,
+                               shard_utterances)
 
 
 def test_shard_covers_and_balances():
@@ -22,6 +25,42 @@ def test_shard_covers_and_balances():
     assert shard_utterances(lengths, 2, 0) == shard_utterances(lengths, 2, 0)
 
 
+def test_c4_corpus_is_100h_length_mixed():
+    s = c4_corpus()
+    assert len(s) == C4_UTTS == 36000
+    assert s.sum() == 36000 * 160000                     # exactly 100 h at 16 kHz
+    assert s.min() >= 32000 and s.max() <= 288000         # 2 .. 18 s
+    assert len(np.unique(s)) > 10000                      # a real length mix
+    frames = sum(num_frames(int(n)) for n in s)
+    assert abs(frames - 35.93e6) < 0.01 * 35.93e6         # 35.93 M frames
+    assert np.array_equal(c4_corpus(), s)                 # seeded
+
+
+def test_c4_shards_and_batches():
+    s = c4_corpus(2000)
+    frames = [num_frames(int(n)) for n in s]
+    for world in (1, 2, 8):
+        seen = []
+        loads = []
+        for r in range(world):
+            mine = shard_utterances(frames, world, r)
+            batches = pack_batches([frames[u] for u in mine], 10, 10, 4096)
+            for b in batches:
+                assert sum(frames[mine[i]] + 20 for i in b) <= 4096
+                seen += [mine[i] for i in b]
+            loads.append(sum(frames[u] for u in mine))
+        assert sorted(seen) == list(range(len(s)))
+        assert max(loads) - min(loads) <= max(frames)
+
+
+def test_pack_batches_edges():
+    assert pack_batches([], 1, 1) == []
+    assert pack_batches([0, 5, 0], 1, 1, 10) == [[1]]
+    # an utterance longer than a batch still gets one (the plan splits it)
+    assert pack_batches([3, 20, 3], 1, 1, 10) == [[0], [1], [2]]
+    assert pack_batches([3, 3, 3], 1, 1, 10) == [[0, 1], [2]]
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -30,40 +69,60 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, steps, q):
+def _rows(rank, step, n, width):
+    # distinct values in every row and column, so a row lost or moved shows
+    return (1000.0 * rank + 10.0 * step + np.arange(n)[:, None] + 0.001 * np.arange(width)[None, :]).astype(np.float32)
+
+
+def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        g = LoglikGather((5, 7), torch.float32, "cpu", depth=3)
-        bufs = [torch.empty(5, 7) for _ in range(3)]
-        for i in range(steps):
-            o = i % 3
-            g.wait_slot(o)
-            bufs[o].fill_(1000.0 * rank + i)  # row 0 sums to 7 * value
-            assert g.submit(bufs[o]) == o
-        total = g.drain()
-        q.put((rank, float(total), g.batches))
+        width = 7
+        # ragged per-rank batch lists: rank 1 has one step more, and a step
+        # with no rows at all
+        mine = {0: [5, 3, 4], 1: [2, 6, 0, 1]}[rank]
+        counts = exchange_counts(mine)
+        g = RowGather(counts, width, torch.float32, "cpu", depth=2, keep=True)
+        bufs = [torch.empty(8, width) for _ in range(2)]
+        steps = max(len(c) for c in counts)
+        for s in range(steps):
+            slot = s % 2
+            g.wait_slot(slot)
+            n = mine[s] if s < len(mine) else 0
+            if n:
+                bufs[slot][:n] = torch.from_numpy(_rows(rank, s, n, width))
+            own = bufs[slot][:n] if rank == 0 and n else None
+            assert g.submit(s, bufs[slot], own=own) == slot
+        total = float(g.drain())
+        kept = [(p, s, a.tolist()) for p, s, a in (g.keep or [])]
+        q.put((rank, total, g.rows_in, kept))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_streamed_gather_gloo(world):
-    steps = 7
+def test_row_gather_gloo_ragged():
+    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, steps, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict()
+    res = {}
     for _ in range(world):
-        r, total, batches = q.get(timeout=120)
-        res[r] = (total, batches)
+        r, total, rows_in, kept = q.get(timeout=120)
+        res[r] = (total, rows_in, kept)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    expect = sum(7.0 * (1000.0 * r + i) for r in range(world) for i in range(steps))
-    assert res[0][0] == pytest.approx(expect)
-    assert all(b == steps for _, b in res.values())
+    counts = {0: [5, 3, 4], 1: [2, 6, 0, 1]}
+    want = sum(float(_rows(r, s, n, 7).astype(np.float64).sum()) for r in counts for s, n in enumerate(counts[r]) if n)
+    assert res[0][0] == pytest.approx(want, rel=1e-12)
+    assert res[0][1] == 2 + 6 + 1
+    # every received row, full width, exactly the sender's
+    got = {(p, s): np.array(a, np.float32) for p, s, a in res[0][2]}
+    assert sorted(got) == [(1, 0), (1, 1), (1, 3)]
+    for (p, s), a in got.items():
+        assert np.array_equal(a, _rows(p, s, counts[p][s], 7))

@@ -225,13 +225,16 @@ def test_am_batcher_device_failure_releases_every_stream(tmp_path, xs_config):
     args = []
     for i, f in enumerate(feats):
         args += [_put(tmp_path, f"x{i}.f32", f), len(f)]
-    conf = _am_config(tmp_path, xs_config, 50, extra="gpu_batch_streams = 4\ngpu_batch_wait_us = 3000\n")
+    # the leader waits (up to 20 s) until all four streams have enqueued, so
+    # the failing first call carries four requests: the three followers must
+    # be released with the leader's error, not just the leader
+    conf = _am_config(tmp_path, xs_config, 50, extra="gpu_batch_streams = 4\ngpu_batch_wait_us = 20000000\n")
     r = subprocess.run([DRIVER, "am_mt_fail", str(conf), str(tmp_path / "mt")] + [str(a) for a in args],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     calls, blocks, failed = [int(v) for v in r.stdout.split()[1::2]]
-    assert 1 <= failed <= len(feats)
-    assert calls >= 1
+    assert failed == len(feats) > 1
+    assert calls == 1 and blocks == len(feats)
     # the streams outside the failed batch completed with full output
     done = [i for i in range(len(feats)) if (tmp_path / f"mt{i}.bin").exists()]
     assert len(done) == len(feats) - failed
