@@ -47,6 +47,9 @@ $(OBJ)/gemm_bf16x6.o $(OBJ)/gemm_f16x3.o: HIPFLAGS += -mllvm -disable-promote-al
 # VALU costs more issue cycles than the scalar pair in an MFMA gap)
 $(OBJ)/gemm_bf16x6.o: HIPFLAGS += -fno-slp-vectorize $(X6FLAGS)
 
+# the fast fbank mode is not bit-exact by design: let it contract mul/add
+$(OBJ)/fbank_fast.o: HIPFLAGS += -ffp-contract=fast
+
 $(OBJ)/%.o: $(SRC)/kernels/%.hip $(HDRS)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@

@@ -82,6 +82,9 @@ def parse():
     ap.add_argument("--c4-dump", default=None,
                     help="c4, tests only: rank 0 writes every gathered row (and its own) per utterance "
                          "to this .npz (small corpora)")
+    ap.add_argument("--fbank", choices=["exact", "fast"], default="exact",
+                    help="fbank kernel (ce_gpu_ctx_set_fbank): exact = the reference's operation order "
+                         "(bit-exact pre-log mel), fast = four-step FFT within 3e-5 on log-mel")
     ap.add_argument("--pcm", choices=["f32", "s16"], default="f32",
                     help="resident PCM format: f32 (raw int16 scale floats, WaveReader's output) or s16 "
                          "(the WAV payload; ce_gpu_fbank_s16 converts exactly in the kernel)")
@@ -303,6 +306,7 @@ def main_c2(args):
     n_utt, n_samp = 1000, int(16000 * args.seconds)
     stream = torch.cuda.current_stream()
     ctx = gpu.Context(local, stream)
+    ctx.set_fbank(args.fbank)
     plan = gpu.Plan(ctx, [n_samp] * n_utt)
     s16 = args.pcm == "s16"
     pcm = torch.empty((n_utt, n_samp), dtype=torch.int16 if s16 else torch.float32, device="cuda")
@@ -345,10 +349,11 @@ def main_c2(args):
     if iv:
         avg_ms = sum(b - a for a, b in iv) / len(iv)
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-        traffic, src = pmc_traffic("fbank_kernel", "c2")
+        kname = "fbank_fast_kernel" if args.fbank == "fast" else "fbank_kernel"
+        traffic, src = pmc_traffic(kname, "c2")
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
-                    "kernel": "fbank_kernel", "launches": len(iv), "avg_launch_ms": round(avg_ms, 4),
+                    "kernel": kname, "launches": len(iv), "avg_launch_ms": round(avg_ms, 4),
                     "algorithmic_bytes_per_launch": bytes_per_launch,
                     "valu_flops_per_frame": 14000}
     cpu = None
@@ -368,6 +373,7 @@ def main_c2(args):
         "data": "synthetic (seeded 16 kHz PCM at raw int16 scale)",
         "config": {"workload": f"C2 batched fbank only, {n_utt} x {args.seconds:g} s utterances per step per GPU",
                    "pcm": "int16 (WAV payload)" if s16 else "float32 at raw int16 scale",
+                   "fbank": args.fbank,
                    "frames_per_step_per_gpu": plan.total_frames, "parallelism": f"utterance shard x{world}"},
         "roofline": roofline, "cpu_baseline": cpu, "checksum": checksum,
     }
@@ -415,6 +421,7 @@ def main_c4(args):
     front = backs[0] if args.serial else torch.cuda.Stream()
     ctxs = [gpu.Context(local, b) for b in backs]
     ctx_f = ctxs[0] if args.serial else gpu.Context(local, front)
+    ctx_f.set_fbank(args.fbank)
     model = gpu.Model(ctxs[0], conf)
     if args.gemm:
         model.set_gemm(args.gemm)
@@ -659,6 +666,8 @@ def main():
     ctxs = [gpu.Context(local, b) for b in backs]
     ctx = ctxs[0]
     ctx_fs = [gpu.Context(local, f) for f in fronts] if not args.serial else [ctx]
+    for c in ctx_fs:
+        c.set_fbank(args.fbank)
     int8 = args.workload == "c5"
     model = gpu.Model(ctx, conf)
     if args.gemm:
@@ -914,7 +923,7 @@ def main():
                                f"({U} x {args.seconds:g} s utterances/step/GPU)" +
                                ("" if not gather else "; C4 RCCL gather of log-likelihoods to rank 0"),
                    "frames_per_step_per_gpu": frames_per_step, "packed_rows": plan.max_chunk_rows,
-                   "cmvn": not args.no_cmvn, "parallelism": f"utterance shard x{world}",
+                   "cmvn": not args.no_cmvn, "fbank": args.fbank, "pcm": args.pcm, "parallelism": f"utterance shard x{world}",
                    "streams": 1 if args.serial else 1 + NB,
                    "gather": gather},
         "roofline": roofline, "cpu_baseline": cpu, "stages": stages,

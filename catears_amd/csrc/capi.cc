@@ -303,6 +303,31 @@ static int upload_split(const std::vector<float> &wt, int n, int kpad, DevBuf *o
   return out->upload(sp.data(), sp.size() * 2);
 }
 
+// The direct-weight kernel's image (X6Gemm::wd): the same three planes in
+// MFMA A-fragment order, units zero-padded to a multiple of kX6DirUnits.
+static int upload_wdir(const std::vector<float> &wt, int n, int kpad, DevBuf *out) {
+  const int npad = (n + kX6DirUnits - 1) / kX6DirUnits * kX6DirUnits, kt = kpad / 32;
+  std::vector<uint16_t> img((size_t)npad * 3 * kpad, 0);
+  for (int ub = 0; ub < npad / 16; ++ub)
+    for (int t = 0; t < kt; ++t)
+      for (int l = 0; l < 64; ++l) {
+        const int j = ub * 16 + (l & 15), k0 = t * 32 + (l >> 4) * 8;
+        if (j >= n) continue;
+        for (int e = 0; e < 8; ++e) {
+          const float v = wt[(size_t)j * kpad + k0 + e];
+          const uint16_t h = bf16_rne(v);
+          const float r1 = v - bf16_float(h);
+          const uint16_t m = bf16_rne(r1);
+          const uint16_t lo = bf16_rne(r1 - bf16_float(m));
+          const size_t base = (((size_t)ub * kt + t) * 3) * 512 + (size_t)l * 8 + e;
+          img[base] = h;
+          img[base + 512] = m;
+          img[base + 1024] = lo;
+        }
+      }
+  return out->upload(img.data(), img.size() * 2);
+}
+
 // fp32 -> fp16 bits, round to nearest even (v_cvt_f16_f32), inf beyond 65504.
 static uint16_t f16_rne(float f) {
   uint32_t x;
@@ -434,6 +459,7 @@ static int build_program(const std::vector<RawLayer> &layers, int left, int righ
           for (int j = 0; j < out; ++j) wt[(size_t)j * g.kpad + k] = L.w[(size_t)k * out + j];
         CE_TRY(g.wt.upload(wt.data(), wt.size() * 4));
         CE_TRY(upload_split(wt, out, g.kpad, &g.wsplit));
+        if (g.kpad % 32 == 0) CE_TRY(upload_wdir(wt, out, g.kpad, &g.wdir));
         bool f16_ok = false;
         CE_TRY(upload_f16(wt, out, g.kpad, &g.wf16, &g.w_shift, &f16_ok));
         if (!f16_ok) m->x3_ok = false;
@@ -712,6 +738,13 @@ int ce_gpu_ctx_set_latency(ce_gpu_ctx *ctx, int on) {
   return CE_GPU_OK;
 }
 
+int ce_gpu_ctx_set_fbank(ce_gpu_ctx *ctx, int mode) {
+  if (!ctx) return fail(CE_GPU_EINVAL, "NULL argument");
+  if (mode != CE_GPU_FBANK_EXACT && mode != CE_GPU_FBANK_FAST) return fail(CE_GPU_EINVAL, "unknown fbank mode");
+  ctx->fbank_mode = mode;
+  return CE_GPU_OK;
+}
+
 int ce_gpu_ctx_synchronize(ce_gpu_ctx *ctx) {
   if (!ctx) return fail(CE_GPU_EINVAL, "ctx is NULL");
   CE_HIP(hipStreamSynchronize(ctx->stream));
@@ -985,13 +1018,17 @@ int ce_gpu_plan_destroy(ce_gpu_plan *p) {
 int ce_gpu_fbank(ce_gpu_ctx *ctx, const ce_gpu_plan *p, const float *d_pcm, float *d_feats, float *d_mel) {
   if (!ctx || !p || (p->total_frames > 0 && (!d_pcm || !d_feats))) return fail(CE_GPU_EINVAL, "NULL argument");
   ProfScope prof(ctx, CE_GPU_PROF_FBANK);
-  return launch_fbank(ctx->stream, ctx->d_tables.as<FbankTables>(), p, d_pcm, d_feats, d_mel);
+  const FbankTables *t = ctx->d_tables.as<FbankTables>();
+  return ctx->fbank_mode == CE_GPU_FBANK_FAST ? launch_fbank_fast(ctx->stream, t, p, d_pcm, d_feats, d_mel)
+                                              : launch_fbank(ctx->stream, t, p, d_pcm, d_feats, d_mel);
 }
 
 int ce_gpu_fbank_s16(ce_gpu_ctx *ctx, const ce_gpu_plan *p, const int16_t *d_pcm, float *d_feats, float *d_mel) {
   if (!ctx || !p || (p->total_frames > 0 && (!d_pcm || !d_feats))) return fail(CE_GPU_EINVAL, "NULL argument");
   ProfScope prof(ctx, CE_GPU_PROF_FBANK);
-  return launch_fbank_s16(ctx->stream, ctx->d_tables.as<FbankTables>(), p, d_pcm, d_feats, d_mel);
+  const FbankTables *t = ctx->d_tables.as<FbankTables>();
+  return ctx->fbank_mode == CE_GPU_FBANK_FAST ? launch_fbank_fast_s16(ctx->stream, t, p, d_pcm, d_feats, d_mel)
+                                              : launch_fbank_s16(ctx->stream, t, p, d_pcm, d_feats, d_mel);
 }
 
 int ce_gpu_cmvn(ce_gpu_ctx *ctx, const ce_gpu_plan *p, const float *d_global_stats, const float *d_feats,
@@ -1174,6 +1211,8 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
     a.ldw = g.kpad;
     a.w = g.wsplit.as<uint16_t>();  // the same weights as planes (kernels that read them)
     a.pw = g.kpad;
+    a.wd = g.wdir.as<uint16_t>();   // and as MFMA fragments (the default kernel)
+    a.wd_kt = g.kpad / 32;
     a.m = rows;
     a.n = g.n;
     a.kpad = i == 0 ? g.kpad : g.nseg * g.din;

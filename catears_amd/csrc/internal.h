@@ -84,6 +84,11 @@ struct FbankTables {
   int mel_wbase[kMel];              // start of its weights in mel_w
   float mel_w[512];                 // 492 nonzero weights in total
   int mel_total;
+  // fast mode (kernels/fbank_fast.hip: four-step 16 x 16 FFT, 16 lanes per
+  // frame; not the reference's operation order, <= 3e-5 on log-mel)
+  float ff_tw[16 * 16 * 2];         // W256^(n2 k1) = (cos, -sin)(2 pi n2 k1 / 256) at [k1][n2]
+  float ff_post[kHalf * 2];         // W512^k = (cos, -sin)(2 pi k / 512), k = 0..255
+  int ff_lane_band[16 * 4];         // mel bands formed by each of a frame's 16 lanes (-1: none)
 };
 
 // Builds the tables (tables.cc).
@@ -162,6 +167,7 @@ struct GemmLayer {
   DevBuf wt;              // n x kpad, K-contiguous (transposed MAT0)
   DevBuf wsplit;          // n x 3*kpad bf16: wt as three planes (bf16x6 GEMM)
   DevBuf wf16;            // n x 2*kpad fp16: wt * 2^w_shift as two planes (f16x3 GEMM)
+  DevBuf wdir;            // wt's planes in MFMA A-fragment order (X6Gemm::wd), units padded to 256
   int w_shift = 0;
   DevBuf bias;            // n
   DevBuf bn_scale, bn_offset;  // n, when a BatchNorm is fused
@@ -225,6 +231,7 @@ struct ce_gpu_ctx {
   catears::DevBuf blk_maps;    // ce_gpu_nnet_propagate_blocks: row_dst + row_edge
   catears::DevBuf overflow;    // int: an f16x3 split left the fp16 range (ce_gpu_ctx_overflow)
   int latency = 0;             // ce_gpu_ctx_set_latency: split-K GEMMs for small batches
+  int fbank_mode = 0;          // ce_gpu_ctx_set_fbank: CE_GPU_FBANK_EXACT / _FAST
   catears::DevBuf split_part;  // latency mode: GEMM partials (grown on demand)
   catears::DevBuf split_ticket;  // latency mode: per-tile arrival counters (zeroed when grown)
   std::vector<int32_t> h_blk_maps;
@@ -314,6 +321,11 @@ int launch_fbank(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, 
                  float *feats, float *mel);
 int launch_fbank_s16(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, const int16_t *pcm,
                      float *feats, float *mel);
+// fast mode (ce_gpu_ctx_set_fbank(ctx, CE_GPU_FBANK_FAST))
+int launch_fbank_fast(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, const float *pcm,
+                      float *feats, float *mel);
+int launch_fbank_fast_s16(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, const int16_t *pcm,
+                          float *feats, float *mel);
 int launch_cmvn(hipStream_t s, const ce_gpu_plan *p, const float *gstats, const float *in,
                 float *out);
 
@@ -351,6 +363,13 @@ struct X6Gemm {
   // K-contiguous): split into the three planes on the way into LDS; the
   // output is then fp32 (y32) for every layer
   const float *xf = nullptr, *wf = nullptr;
+  // the same weights as MFMA A fragments (gemm_bf16x6d_kernel, the default
+  // with fp32 activations): for 16-unit block u, K-tile t (32 k) and plane p
+  // the 1 KB at ((u * wd_kt + t) * 3 + p) * 512 elements holds lane l's 8
+  // bf16 (unit 16 u + (l & 15), k = 32 t + 8 (l >> 4) ..+7) at 8 l; units
+  // zero-padded to a multiple of kX6DirUnits
+  const uint16_t *wd = nullptr;
+  int wd_kt = 0;
   int m = 0, n = 0, kpad = 0, din = 0, nseg = 1;
   int off[8] = {0};
   const float *bias = nullptr, *bn_scale = nullptr, *bn_offset = nullptr;
@@ -368,6 +387,7 @@ struct X6Gemm {
   size_t split_tiles = 0;
 };
 int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a);
+constexpr int kX6DirUnits = 256;  // gemm_bf16x6d_kernel's unit tile
 size_t x6_split_part_floats(int m, int n, int splitk);
 size_t x6_split_tiles(int m, int n);
 // latency-mode GEMMs run in launches of at most this many rows (bounds the

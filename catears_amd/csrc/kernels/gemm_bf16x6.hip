@@ -72,6 +72,8 @@ struct X6Args {
   unsigned *ticket;  // split-K: arrival counter per tile, zero between launches
   int splitk;
   int row0;          // split-K: first row of this launch's row window
+  const uint16_t *wd;  // weights as MFMA A fragments (gemm_bf16x6d_kernel), see X6Gemm::wd
+  int wd_kt;           // K-tiles per 16-unit block in that image
 };
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
@@ -719,6 +721,163 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
   x6_epilogue<TW, TF, false>(p, acc, n0 + wrow, f0 + frow, lane);
 }
 
+// Direct-weight schedule (the default): the constant weights are split into
+// their three bf16 planes once, at model load, and stored in the order the
+// MFMA reads its A operand (X6Gemm::wd: per 16-unit block, K-tile and plane
+// one contiguous 1 KB fragment, lane l's 16 bytes at 16 l).  Each wave loads
+// its weight fragments straight from L2 into registers with one
+// global_load_dwordx4 per fragment -- no split VALU, no LDS write and no LDS
+// read for the weights -- so LDS carries only the activations, split once per
+// block on their way in (as gemm_bf16x6f_kernel does).  Per K-tile and CU
+// that removes 2/3 of the ds_write_b128 traffic, half the fragment reads and
+// 2/3 of the split VALU of the fp32-operand kernel, whose ablations placed its
+// overhead over the bare MFMA loop in exactly that LDS-write path (DESIGN.md
+// §8).  Tile: BW = 256 units x BF = 128 frames, 8 waves of 64 x 64 (4 along
+// the units, 2 along the frames: each weight fragment is loaded by two waves,
+// the second from L1).  Products, their order per output element and the
+// planes are those of gemm_bf16x6f_kernel, so results are bit-identical to
+// it.  Per K-tile, in order (the weights of tile kt+1 are issued as soon as
+// tile kt's registers are free: a0 one tile ahead in a second buffer, a1
+// after its last product, a2 at the end of the tile):
+//   read b0 b1 (planes 0, 1 of the activations) | load a0 of kt+1 |
+//   16 MFMAs a0 b0 | split + write activation tile kt+1, load tile kt+2 |
+//   48 MFMAs a0 b1, a1 b0, a1 b1 | read b2 | load a1 of kt+1 |
+//   32 MFMAs a0 b2, a2 b0 | load a2 of kt+1 | lgkmcnt(0), barrier.
+//   WAR: activation stage (kt+1) % 2 was last read in tile kt-1, before the
+//        barrier that closed it; RAW: its writes precede the barrier that
+//        closes tile kt.
+template <class C>
+__global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
+  constexpr int BF = C::BF, TW = C::TW, TF = C::TF, NT = C::NT;
+  constexpr int RPP = NT / 4;  // activation rows per pass (4 threads x 32 B per row)
+  static_assert(BF == RPP, "one activation row chunk per thread");
+  constexpr int ASTAGE = 3 * BF * 64;  // bytes: one K-tile of activation planes
+  __shared__ __attribute__((aligned(1024))) char smem[2 * ASTAGE];
+  auto swz = [](int row) { return ((row >> 3) & 1) << 1; };
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef const __attribute__((address_space(1))) f32x4v gvec;
+  typedef const __attribute__((address_space(1))) bf16x8 gfrag;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ww = wave / C::WGF, wf = wave % C::WGF;
+  int tm, tn;
+  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
+  const int f0 = tm * BF, n0 = tn * C::BW;
+  const int prow = tid >> 2, pch = tid & 3;
+  const int ktiles = p.kpad / 32;
+
+  // weight fragment i of this wave: 16-unit block (n0 + 64 ww + 16 i) / 16
+  gfrag *wb[TW];
+#pragma unroll
+  for (int i = 0; i < TW; ++i)
+    wb[i] = (gfrag *)(p.wd + ((size_t)((n0 >> 4) + ww * TW + i) * p.wd_kt * 3 * 64 + lane) * 8);
+  auto load_w = [&](int kt, int pl, bf16x8 *dst) {
+    kt = min(kt, ktiles - 1);
+#pragma unroll
+    for (int i = 0; i < TW; ++i) dst[i] = wb[i][(kt * 3 + pl) * 64];
+  };
+  f32x4v rx0[2], rx1[2];  // activation row chunks of tiles kt+1 / kt+2 (by parity)
+  auto load_x = [&](int kt, int r) {
+    kt = min(kt, ktiles - 1);
+    const int k0 = kt * 32;
+    const int seg = k0 / p.din, col0 = k0 - seg * p.din;
+    const int shift = (int)(signed char)(p.off_packed >> (8 * seg));
+    gvec *xb = (gvec *)(p.xf + col0 + 8 * pch);
+    const int src = clampi(f0 + prow + shift, 0, p.m - 1);
+    const uint32_t o = (uint32_t)(src * p.ldx) / 4;
+    rx0[r] = xb[o];
+    rx1[r] = xb[o + 1];
+  };
+  auto put = [&](char *st, int r) {
+    const Planes2 q0 = split3_pair(rx0[r].x, rx0[r].y), q1 = split3_pair(rx0[r].z, rx0[r].w);
+    const Planes2 q2 = split3_pair(rx1[r].x, rx1[r].y), q3 = split3_pair(rx1[r].z, rx1[r].w);
+    const int off = prow * 64 + ((pch ^ swz(prow)) * 16);
+    *reinterpret_cast<u32x4 *>(st + off) = u32x4{q0.h, q1.h, q2.h, q3.h};
+    *reinterpret_cast<u32x4 *>(st + BF * 64 + off) = u32x4{q0.m, q1.m, q2.m, q3.m};
+    *reinterpret_cast<u32x4 *>(st + 2 * BF * 64 + off) = u32x4{q0.l, q1.l, q2.l, q3.l};
+  };
+  const int foff = (lane & 15) * 64 + (((lane >> 4) ^ (((lane >> 3) & 1) << 1)) * 16);
+  const int frow = wf * TF * 16;
+  auto read_b = [&](const char *st, int pl, bf16x8 *b) {
+#pragma unroll
+    for (int j = 0; j < TF; ++j) b[j] = *reinterpret_cast<const bf16x8 *>(st + (pl * BF + frow + j * 16) * 64 + foff);
+  };
+
+  f32x4 acc[TW][TF];
+#pragma unroll
+  for (int i = 0; i < TW; ++i)
+#pragma unroll
+    for (int j = 0; j < TF; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+
+  bf16x8 a0[2][TW], a1[TW], a2[TW], b0[TF], b1[TF], b2[TF];
+  load_x(0, 0);
+  load_w(0, 0, a0[0]);
+  load_w(0, 1, a1);
+  load_w(0, 2, a2);
+  put(smem, 0);
+  load_x(1, 1);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  auto body = [&](int kt, auto cc) {
+    constexpr int c = decltype(cc)::value;
+    const char *st = smem + (kt & 1) * ASTAGE;
+    char *sn = smem + ((kt + 1) & 1) * ASTAGE;
+    // Regions (sched_barrier): the compiler would otherwise sink every load
+    // to its registers' last use and then wait on it at the next tile's
+    // head.  The loads sit in regions of their own at the top of the
+    // phase after their registers' last use; the split VALU of the next
+    // activation tile shares the 48-MFMA region so it interleaves.
+    // Activation registers alternate by tile parity: tile kt+1's chunk
+    // (loaded one tile ago) is written while tile kt+2's is loaded.
+    read_b(st, 0, b0);
+    read_b(st, 1, b1);
+    load_w(kt + 1, 0, a0[c ^ 1]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < TW; ++i)
+#pragma unroll
+      for (int j = 0; j < TF; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[c][i], b0[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    load_x(kt + 2, c);
+    __builtin_amdgcn_sched_barrier(0);
+    put(sn, c ^ 1);
+#pragma unroll
+    for (int i = 0; i < TW; ++i)
+#pragma unroll
+      for (int j = 0; j < TF; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[c][i], b1[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b0[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b1[j], acc[i][j], 0, 0, 0);
+      }
+    read_b(st, 2, b2);
+    __builtin_amdgcn_sched_barrier(0);
+    load_w(kt + 1, 1, a1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < TW; ++i)
+#pragma unroll
+      for (int j = 0; j < TF; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[c][i], b2[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2[i], b0[j], acc[i][j], 0, 0, 0);
+      }
+    __builtin_amdgcn_sched_barrier(0);
+    load_w(kt + 1, 2, a2);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  int kt = 0;
+  for (; kt + 1 < ktiles; kt += 2) {
+    body(kt, std::integral_constant<int, 0>());
+    body(kt + 1, std::integral_constant<int, 1>());
+  }
+  if (kt < ktiles) body(kt, std::integral_constant<int, 0>());
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail prefetches
+  x6_epilogue<TW, TF, false>(p, acc, n0 + ww * TW * 16, f0 + frow, lane);
+}
+
 // Warp-specialised fp32-in schedule: the block is C::NW MFMA waves plus
 // NPV producer waves.  The producers do all the global loads, splits and
 // plane writes of tile kt+1 while the MFMA waves read and multiply tile kt,
@@ -916,6 +1075,16 @@ int launch_f(hipStream_t s, X6Args p) {
   return CE_GPU_OK;
 }
 
+template <class C>
+int launch_d(hipStream_t s, X6Args p) {
+  p.tiles_n = (p.n + C::BW - 1) / C::BW;
+  p.tiles_m = (p.m + C::BF - 1) / C::BF;
+  dim3 grid(p.tiles_m * p.tiles_n), block(C::NT);
+  hipLaunchKernelGGL((gemm_bf16x6d_kernel<C>), grid, block, 0, s, p);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
 template <class C, int NPV>
 int launch_ws(hipStream_t s, X6Args p) {
   p.tiles_n = (p.n + C::BW - 1) / C::BW;
@@ -964,9 +1133,11 @@ typedef X6Cfg<128, 64, 2, 2, 2> X6LatSmallCfg;
 constexpr int kX6LatSmallRows = 256;
 constexpr int kX6LatSmallPad = 82 * 1024 - 2 * X6LatSmallCfg::STAGE;
 
-// CATEARS_X6_VARIANT: the schedule of the default (fp32-operand) kernel.
-// The product build carries the default (0 = 160, region-scheduled 128 x 256
-// tiles) and the two documented deployment alternatives, all bit-identical
+// CATEARS_X6_VARIANT: the schedule of the fp32-activation bf16x6 GEMM.
+// The product build carries the default (0 = 300, direct weights: 256 x 128
+// tiles, weight fragments straight from L2 to registers), the round-2
+// default 160 (region-scheduled 128 x 256 tiles, weights split in the
+// kernel) and the two documented deployment alternatives, all bit-identical
 // (tests/test_gpu_x6_variants.py): 40 (128 x 128 tiles, one batch at a time
 // on an idle GPU) and 200 (warp-specialised 128 x 128).  Measurement
 // variants -- and the DIAG ablations, which give wrong results -- exist only
@@ -1038,6 +1209,8 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
   p.ticket = nullptr;
   p.splitk = 1;
   p.row0 = 0;
+  p.wd = a.wd;
+  p.wd_kt = a.wd_kt;
   const bool out16 = a.y16 != nullptr;
   if (f32in && a.splitk > 1)
     return a.m <= kX6LatSmallRows ? launch_f_split<X6LatSmallCfg, kX6LatSmallPad>(s, p, a)
@@ -1045,7 +1218,14 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
   if (f32in) {
     switch (x6_variant()) {
       case 0:
-      case 160:  // region-scheduled loop (the default)
+      case 300:  // direct weights (the default when the model carries the fragment image)
+        if (a.wd) {
+          if (a.wd_kt * 32 < a.kpad || (reinterpret_cast<uintptr_t>(a.wd) & 15))
+            return fail(CE_GPU_EINVAL, "gemm_bf16x6: weight fragment image does not cover K");
+          return launch_d<X6Cfg<kX6DirUnits, 128, 4, 2, 2>>(s, p);
+        }
+        [[fallthrough]];
+      case 160:  // region-scheduled fp32-operand loop (round-2 default)
         return launch_f<X6Cfg<128, 256, 2, 4, 2>, 8>(s, p);
       case 40:  // 128 x 128 tiles: fills all CUs on a 1024-wide layer (one batch at a time on an idle GPU)
         return launch_f<X6Cfg<128, 128, 4, 2, 2>>(s, p);
@@ -1086,7 +1266,7 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
 #endif
       default:
         return fail(CE_GPU_EINVAL, "CATEARS_X6_VARIANT=" + std::to_string(x6_variant()) +
-                                       " is not a schedule of this build (product: 0, 40, 200; others need "
+                                       " is not a schedule of this build (product: 0, 300, 160, 40, 200; others need "
                                        "`make EXPERIMENTS=1`)");
     }
   }

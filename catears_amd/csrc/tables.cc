@@ -15,6 +15,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "fbank_ops.h"
@@ -180,6 +181,39 @@ void build_fft_lanes(FbankTables *t) {
   }
 }
 
+// Fast-mode tables: the four-step FFT's inter-pass twiddles, the real-FFT
+// post twiddles (both in double, rounded once) and a balanced assignment of
+// the 40 mel bands to the 16 lanes of a frame (longest band first onto the
+// least-loaded lane, by weight count).
+void build_fast(FbankTables *t) {
+  const double tau = 6.283185307179586476925286766559005;
+  for (int k1 = 0; k1 < 16; ++k1)
+    for (int n2 = 0; n2 < 16; ++n2) {
+      const double a = tau * n2 * k1 / 256.0;
+      t->ff_tw[2 * (k1 * 16 + n2)] = (float)cos(a);
+      t->ff_tw[2 * (k1 * 16 + n2) + 1] = (float)-sin(a);
+    }
+  for (int k = 0; k < kHalf; ++k) {
+    const double a = tau * k / 512.0;
+    t->ff_post[2 * k] = (float)cos(a);
+    t->ff_post[2 * k + 1] = (float)-sin(a);
+  }
+  int load[16] = {0}, count[16] = {0};
+  for (int i = 0; i < 16 * 4; ++i) t->ff_lane_band[i] = -1;
+  std::vector<int> order(kMel);
+  for (int b = 0; b < kMel; ++b) order[b] = b;
+  std::sort(order.begin(), order.end(), [&](int a, int b) {
+    return t->mel_len[a] != t->mel_len[b] ? t->mel_len[a] > t->mel_len[b] : a < b;
+  });
+  for (int b : order) {
+    int best = -1;
+    for (int l = 0; l < 16; ++l)
+      if (count[l] < 4 && (best < 0 || load[l] < load[best])) best = l;
+    t->ff_lane_band[best * 4 + count[best]++] = b;
+    load[best] += t->mel_len[b];
+  }
+}
+
 }  // namespace
 
 void build_fbank_tables(FbankTables *t) {
@@ -190,6 +224,7 @@ void build_fbank_tables(FbankTables *t) {
   build_post_twiddles(t);
   build_fft_schedule(t);
   build_fft_lanes(t);
+  build_fast(t);
 }
 
 }  // namespace catears

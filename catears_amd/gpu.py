@@ -31,7 +31,7 @@ ABI = [
     "ce_gpu_profile_anchor", "ce_gpu_ctx_profile_intervals", "ce_gpu_model_quantize",
     "ce_gpu_nnet_propagate_blocks", "ce_gpu_loglik_gather", "ce_gpu_loglik_columns",
     "ce_gpu_model_set_gemm", "ce_gpu_model_get_gemm", "ce_gpu_ctx_overflow", "ce_gpu_ctx_set_latency",
-    "ce_gpu_fbank_s16", "ce_gpu_score_s16",
+    "ce_gpu_fbank_s16", "ce_gpu_score_s16", "ce_gpu_ctx_set_fbank",
 ]
 
 # ce_gpu_model_set_gemm modes
@@ -102,6 +102,7 @@ def lib():
         "ce_gpu_model_get_gemm": (ci, [vp, pi]),
         "ce_gpu_ctx_overflow": (ci, [vp, pi]),
         "ce_gpu_ctx_set_latency": (ci, [vp, ci]),
+        "ce_gpu_ctx_set_fbank": (ci, [vp, ci]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -149,6 +150,14 @@ class Context:
         """Latency mode (ce_gpu_ctx_set_latency): split-K nnet GEMMs for small
         row blocks scored one at a time."""
         check(lib().ce_gpu_ctx_set_latency(self.h, int(bool(on))))
+
+    FBANK_MODES = {"exact": 0, "fast": 1}
+
+    def set_fbank(self, mode="exact"):
+        """Fbank kernel of this context (ce_gpu_ctx_set_fbank): "exact" (the
+        reference's operation order, bit-exact pre-log energies) or "fast"
+        (four-step FFT, <= 3e-5 on log-mel)."""
+        check(lib().ce_gpu_ctx_set_fbank(self.h, self.FBANK_MODES[mode]))
 
     def overflow(self):
         """True if an f16x3 GEMM met an out-of-range activation since the

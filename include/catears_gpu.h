@@ -59,7 +59,8 @@ const char *ce_gpu_last_error(void);
 /* Library version string, "catears-mi355x <abi> (gfx950)".  ABI history
  * (INTEGRATION.md §5): 0.1 round 1; 0.2 ce_gpu_loglik_gather gained `dim`
  * (argument 5) -- a caller built against 0.1 must be rebuilt; 0.3 adds the
- * int16 PCM entry points (ce_gpu_fbank_s16, ce_gpu_score_s16). */
+ * int16 PCM entry points (ce_gpu_fbank_s16, ce_gpu_score_s16) and the fast
+ * fbank mode (ce_gpu_ctx_set_fbank). */
 const char *ce_gpu_version(void);
 
 /* ------------------------------------------------------------ context --- */
@@ -98,6 +99,18 @@ int ce_gpu_ctx_overflow(ce_gpu_ctx *ctx, int *overflow);
  * Results differ from the default mode's only by fp32 summation order.  Off
  * (0, the default) is the throughput mode for full 4096-row batches. */
 int ce_gpu_ctx_set_latency(ce_gpu_ctx *ctx, int on);
+
+/* Fbank kernel of ctx's ce_gpu_fbank / ce_gpu_fbank_s16 / ce_gpu_score*:
+ *   CE_GPU_FBANK_EXACT (default) the reference's operation order
+ *       (src/fbank.cc:44-245, src/srfft.cc:124-459): pre-log mel energies
+ *       bit-identical to Fbank::Process, log-mel within 1e-5;
+ *   CE_GPU_FBANK_FAST  a four-step 16 x 16 FFT with 16 lanes per frame and
+ *       tabled twiddles: the same features within 3e-5 on the log (measured
+ *       against the oracle and the reference's Kaldi dump, tests), several
+ *       times the exact kernel's frame rate. */
+#define CE_GPU_FBANK_EXACT 0
+#define CE_GPU_FBANK_FAST 1
+int ce_gpu_ctx_set_fbank(ce_gpu_ctx *ctx, int mode);
 
 /* Kernel timing for roofline reporting: while enabled, every launch of the
  * given kernel class is bracketed by a pair of HIP events on the context's

@@ -207,12 +207,29 @@ def nnet_propagate(layers, x, gemm=None):
     return x
 
 
-def nnet_propagate_int8(layers, x):
+def gemm_u8u8f32_f64(a, sa, zpa, b, sb, zpb):
+    """gemm_u8u8f32 (orc_gemm_u8u8f32) for operands too large for its scalar
+    loop: each zero-point-shifted product is an integer of magnitude at most
+    255^2, so while k * 255^2 < 2^31 the int32 accumulator never wraps and a
+    float64 matmul (every partial sum an integer below 2^53) computes it
+    exactly; the float stage is the same float(acc) * (sa * sb) in float32
+    (an exact integer rounded float64 -> float32 is the int32 -> float
+    conversion, both round to nearest even)."""
+    k = a.shape[1]
+    assert k * 255 * 255 < 2 ** 31, "accumulator could wrap: use gemm_u8u8f32"
+    acc = (a.astype(np.float64) - zpa) @ (b.astype(np.float64) - zpb)
+    s = np.float32(np.float32(sa) * np.float32(sb))
+    return (acc.astype(np.float32) * s).astype(np.float32)
+
+
+def nnet_propagate_int8(layers, x, exact_f64=False):
     """Nnet::Propagate with every LinearLayer as Quantize + MatMat_U8U8F32 +
     bias (src/matrix.cc:329-420) -- the int8 path of BASELINE config C5, as
     catears_amd runs it (include/catears_gpu.h ce_gpu_model_quantize): the
     activation parameters come from the block entering the Splice (equal to
-    those of the spliced block, whose rows it all reads), weights per tensor."""
+    those of the spliced block, whose rows it all reads), weights per tensor.
+    exact_f64: the u8 GEMMs through gemm_u8u8f32_f64 (same bits, BLAS speed:
+    C5-sized blocks)."""
     x = np.ascontiguousarray(x, np.float32)
     pre = None  # block entering the pending Splice
     for layer in layers:
@@ -225,7 +242,7 @@ def nnet_propagate_int8(layers, x):
             _, sx, zx = quantize(src)
             xq = _quantize_with(x, sx, zx)
             wq, sw, zw = quantize(layer["W"])
-            y = gemm_u8u8f32(xq, sx, zx, wq, sw, zw)
+            y = (gemm_u8u8f32_f64 if exact_f64 else gemm_u8u8f32)(xq, sx, zx, wq, sw, zw)
             x = (y + np.asarray(layer["b"], np.float32)[None, :]).astype(np.float32)
             pre = None
         else:

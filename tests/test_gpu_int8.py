@@ -113,3 +113,26 @@ def test_int8_tracks_fp32(torch, G, ctx, oracle, xs_config):
     agree = float(np.mean(a.argmax(1) == b.argmax(1)))
     assert agree > 0.5, agree
     assert np.isfinite(b).all()
+
+
+def test_int8_c5_full_batch(torch, G, ctx, oracle):
+    """BASELINE config C5 at its size: TDNN-S int8, one 8192-row block
+    (ce_gpu_nnet_propagate), against the oracle's int8 restatement over the
+    whole block (its u8 GEMMs through the exact float64 form, so every row of
+    every layer -- and hence every per-tensor quantization parameter -- is
+    the reference's).  Without the final LogSoftmax every output bit must
+    match; with it (a float sum in another order) 1e-4."""
+    from catears_amd import formats, synth
+    layers, left, right, _ = synth.tdnn_layers(1024, 3456, seed=7)
+    body = [L for L in layers if L["kind"] != "log_softmax"]
+    x = np.random.default_rng(8192).normal(9.0, 3.0, size=(8192, 40)).astype(np.float32)
+    want = oracle.nnet_propagate_int8(body, x, exact_f64=True)
+    m_body = G.Model(ctx, image=formats.nnet_bytes(body, left, right)).quantize(ctx)
+    got = G.nnet_propagate(ctx, m_body, dev(torch, x)).cpu().numpy()
+    assert got.shape == want.shape == (8192 - left - right, 3456)
+    diff = np.flatnonzero(got.view(np.uint32) != want.view(np.uint32))
+    assert diff.size == 0, f"{diff.size} elements differ, first at {np.unravel_index(diff[0], got.shape)}"
+    m_full = G.Model(ctx, image=formats.nnet_bytes(layers, left, right)).quantize(ctx)
+    got_ls = G.nnet_propagate(ctx, m_full, dev(torch, x)).cpu().numpy()
+    want_ls = oracle.layer_forward({"kind": "log_softmax"}, want)
+    assert np.max(np.abs(got_ls - want_ls)) <= LOGLIK_TOL
