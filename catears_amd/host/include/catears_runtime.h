@@ -2,11 +2,12 @@
 // classes (fbank.h, cmvn.h, nnet.h, am.h, linalg).  Not part of the
 // reference's API; the classes reach the GPU only through include/catears_gpu.h.
 //
-// One ce_gpu context per process on device $CATEARS_DEVICE (default 0) with
-// its own HIP stream.  The reference's hot-path methods are const and may be
-// called from many threads (SURVEY.md 8(b) Threading), so every drop-in call
-// takes Runtime::mutex() for its upload -> kernels -> download sequence and
-// returns with its results on the host, like the CPU code it replaces.
+// ce_gpu contexts on device $CATEARS_DEVICE (default 0), each with its own
+// HIP stream (a "lane").  The reference's hot-path methods are const and may
+// be called from many threads (SURVEY.md 8(b) Threading): every drop-in call
+// holds one lane for its upload -> kernels -> download sequence and returns
+// with its results on the host, like the CPU code it replaces; calls from
+// different threads run on different lanes concurrently.
 // Device failures throw DeviceError (the reference would have crashed on an
 // assert or bad_alloc); there is no CPU fallback.
 #ifndef CATEARS_RUNTIME_H_
@@ -15,6 +16,7 @@
 #include <stddef.h>
 
 #include <mutex>
+#include <utility>
 #include <stdexcept>
 #include <string>
 
@@ -76,11 +78,38 @@ class Runtime {
   // library or the device is unusable.
   static Runtime &Get();
 
-  ce_gpu_ctx *ctx() const { return ctx_; }
-  void *stream() const { return stream_; }
-  std::mutex &mutex() { return mu_; }
+  // Streaming calls from many threads (AcousticModel, Fbank, CMVN) lease a
+  // lane: a context with its own HIP stream and scratch, held exclusively for
+  // one upload -> kernels -> download sequence, so concurrent Instances
+  // overlap their copies and kernels instead of queueing on one mutex.
+  // Lanes are created on demand up to $CATEARS_LANES (default 4, 1..16); a
+  // caller finding every lane busy waits for one.  Device models (weights)
+  // are shared by all lanes of the device.
+  class Lane;
+  class Lease {
+   public:
+    Lease(Lane *lane, std::unique_lock<std::mutex> lock) : lane_(lane), lock_(std::move(lock)) {}
+    ce_gpu_ctx *ctx() const;
+    DeviceBuffer &scratch(int slot);
+    // as Runtime::Upload / Download, on the lane's stream
+    void Upload(void *dst, size_t dst_ld, const void *src, size_t src_ld, size_t elem, size_t rows, size_t cols);
+    void Download(void *dst, size_t dst_ld, const void *src, size_t src_ld, size_t elem, size_t rows, size_t cols);
+    int index() const;
 
-  // Strided 2-D copies on the runtime's stream (element size `elem` bytes,
+   private:
+    Lane *lane_;
+    std::unique_lock<std::mutex> lock_;
+  };
+  Lease Acquire();
+  int lanes_created() const;
+
+  // Lane 0, for the layer-level paths (Nnet / Layer::Propagate, MatMat,
+  // model loading) which take mutex() for their whole sequence.
+  ce_gpu_ctx *ctx() const;
+  void *stream() const;
+  std::mutex &mutex();
+
+  // Strided 2-D copies on lane 0's stream (element size `elem` bytes,
   // leading dimensions in elements).  Upload/CopyDevice are asynchronous;
   // Download waits for the stream.
   void Upload(void *dst, size_t dst_ld, const void *src, size_t src_ld, size_t elem, size_t rows, size_t cols);
@@ -89,18 +118,20 @@ class Runtime {
                   size_t cols);
   void Sync();
 
-  // Per-call scratch (use only while holding mutex()).
-  DeviceBuffer &scratch(int slot) { return scratch_[slot]; }
+  // Per-call scratch of lane 0 (use only while holding mutex()).
+  DeviceBuffer &scratch(int slot);
   static constexpr int kScratchSlots = 6;
 
  private:
   Runtime();
   ~Runtime();
-  ce_gpu_ctx *ctx_ = nullptr;
-  void *stream_ = nullptr;
+  Lane *NewLane();
   int device_ = 0;
-  std::mutex mu_;
-  DeviceBuffer scratch_[kScratchSlots];
+  int max_lanes_ = 4;
+  mutable std::mutex pool_mu_;
+  Lane *lanes_[16] = {nullptr};
+  int n_lanes_ = 0;
+  unsigned next_ = 0;
 };
 
 }  // namespace host

@@ -187,26 +187,26 @@ void AcousticModel::RunBlocks(const std::vector<const float *> &rows, const std:
   const int ctx_rows = left_context_ + right_context_;
   size_t in_rows = 0, out_rows = 0;
   for (int32_t k : n) in_rows += k, out_rows += k - ctx_rows;
-  Runtime &rt = Runtime::Get();
-  std::lock_guard<std::mutex> lock(rt.mutex());
-  float *d_in = static_cast<float *>(rt.scratch(0).Reserve(sizeof(float) * in_rows * dim));
-  float *d_out = static_cast<float *>(rt.scratch(1).Reserve(sizeof(float) * out_rows * pdfs));
+  // a lane of its own: calls from other threads run on other lanes
+  Runtime::Lease lane = Runtime::Get().Acquire();
+  float *d_in = static_cast<float *>(lane.scratch(0).Reserve(sizeof(float) * in_rows * dim));
+  float *d_out = static_cast<float *>(lane.scratch(1).Reserve(sizeof(float) * out_rows * pdfs));
   size_t at = 0;
   for (size_t b = 0; b < rows.size(); ++b) {
-    rt.Upload(d_in + at * dim, dim, rows[b], dim, sizeof(float), n[b], dim);
+    lane.Upload(d_in + at * dim, dim, rows[b], dim, sizeof(float), n[b], dim);
     at += n[b];
   }
-  Check(ce_gpu_ctx_set_latency(rt.ctx(), latency_), "AcousticModel::ComputeBatch");
+  Check(ce_gpu_ctx_set_latency(lane.ctx(), latency_), "AcousticModel::ComputeBatch");
   if (rows.size() == 1)
-    Check(ce_gpu_nnet_propagate(rt.ctx(), model_, d_in, n[0], dim, 1, d_out), "AcousticModel::ComputeBatch");
+    Check(ce_gpu_nnet_propagate(lane.ctx(), model_, d_in, n[0], dim, 1, d_out), "AcousticModel::ComputeBatch");
   else
-    Check(ce_gpu_nnet_propagate_blocks(rt.ctx(), model_, d_in, dim, n.data(), (int)n.size(), 1, d_out),
+    Check(ce_gpu_nnet_propagate_blocks(lane.ctx(), model_, d_in, dim, n.data(), (int)n.size(), 1, d_out),
           "AcousticModel::ComputeBatch");
   at = 0;
   for (size_t b = 0; b < rows.size(); ++b) {
     const int m = n[b] - ctx_rows;
     out[b]->Resize(m, pdfs, Matrix<float>::kUndefined);
-    rt.Download(out[b]->Data(), out[b]->Stride(), d_out + at * pdfs, pdfs, sizeof(float), m, pdfs);
+    lane.Download(out[b]->Data(), out[b]->Stride(), d_out + at * pdfs, pdfs, sizeof(float), m, pdfs);
     at += m;
   }
 }

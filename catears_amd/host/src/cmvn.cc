@@ -23,19 +23,18 @@ CMVN::CMVN(const Vector<float> &global_stats, const Matrix<float> &raw_feats) {
   if (num_frames_ == 0) return;
   // a one-utterance plan whose frame count is num_frames_
   const int64_t samples = CE_GPU_FRAME_LENGTH + (int64_t)CE_GPU_FRAME_SHIFT * (num_frames_ - 1);
-  Runtime &rt = Runtime::Get();
-  std::lock_guard<std::mutex> lock(rt.mutex());
+  Runtime::Lease lane = Runtime::Get().Acquire();
   ce_gpu_plan *raw = nullptr;
-  Check(ce_gpu_plan_create(rt.ctx(), nullptr, &samples, 1, 0, &raw), "CMVN");
+  Check(ce_gpu_plan_create(lane.ctx(), nullptr, &samples, 1, 0, &raw), "CMVN");
   std::unique_ptr<ce_gpu_plan, int (*)(ce_gpu_plan *)> plan(raw, ce_gpu_plan_destroy);
   const size_t n = (size_t)num_frames_ * PK_FBANK_DIM;
-  float *d_in = static_cast<float *>(rt.scratch(0).Reserve(sizeof(float) * n));
-  float *d_out = static_cast<float *>(rt.scratch(1).Reserve(sizeof(float) * n));
-  float *d_stats = static_cast<float *>(rt.scratch(2).Reserve(sizeof(float) * (PK_FBANK_DIM + 1)));
-  rt.Upload(d_in, PK_FBANK_DIM, raw_feats.Data(), raw_feats.Stride(), sizeof(float), num_frames_, PK_FBANK_DIM);
-  rt.Upload(d_stats, PK_FBANK_DIM + 1, global_stats.Data(), PK_FBANK_DIM + 1, sizeof(float), 1, PK_FBANK_DIM + 1);
-  Check(ce_gpu_cmvn(rt.ctx(), plan.get(), d_stats, d_in, d_out), "CMVN");
-  rt.Download(normalized_.data(), PK_FBANK_DIM, d_out, PK_FBANK_DIM, sizeof(float), num_frames_, PK_FBANK_DIM);
+  float *d_in = static_cast<float *>(lane.scratch(0).Reserve(sizeof(float) * n));
+  float *d_out = static_cast<float *>(lane.scratch(1).Reserve(sizeof(float) * n));
+  float *d_stats = static_cast<float *>(lane.scratch(2).Reserve(sizeof(float) * (PK_FBANK_DIM + 1)));
+  lane.Upload(d_in, PK_FBANK_DIM, raw_feats.Data(), raw_feats.Stride(), sizeof(float), num_frames_, PK_FBANK_DIM);
+  lane.Upload(d_stats, PK_FBANK_DIM + 1, global_stats.Data(), PK_FBANK_DIM + 1, sizeof(float), 1, PK_FBANK_DIM + 1);
+  Check(ce_gpu_cmvn(lane.ctx(), plan.get(), d_stats, d_in, d_out), "CMVN");
+  lane.Download(normalized_.data(), PK_FBANK_DIM, d_out, PK_FBANK_DIM, sizeof(float), num_frames_, PK_FBANK_DIM);
 }
 
 CMVN::~CMVN() {}

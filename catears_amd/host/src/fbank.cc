@@ -26,17 +26,16 @@ void Fbank::Process(Instance *inst, const VectorBase<float> &wave, Matrix<float>
   }
   fbank_feature->Resize((int)frames, PK_FBANK_DIM, Matrix<float>::kUndefined);
   {
-    Runtime &rt = Runtime::Get();
-    std::lock_guard<std::mutex> lock(rt.mutex());
+    Runtime::Lease lane = Runtime::Get().Acquire();
     ce_gpu_plan *raw = nullptr;
-    Check(ce_gpu_plan_create(rt.ctx(), nullptr, &samples, 1, 0, &raw), "Fbank::Process");
+    Check(ce_gpu_plan_create(lane.ctx(), nullptr, &samples, 1, 0, &raw), "Fbank::Process");
     std::unique_ptr<ce_gpu_plan, int (*)(ce_gpu_plan *)> plan(raw, ce_gpu_plan_destroy);
-    float *d_pcm = static_cast<float *>(rt.scratch(0).Reserve(sizeof(float) * samples));
-    float *d_feat = static_cast<float *>(rt.scratch(1).Reserve(sizeof(float) * frames * PK_FBANK_DIM));
-    rt.Upload(d_pcm, samples, buf.data(), samples, sizeof(float), 1, samples);
-    Check(ce_gpu_fbank(rt.ctx(), plan.get(), d_pcm, d_feat, nullptr), "Fbank::Process");
-    rt.Download(fbank_feature->Data(), fbank_feature->Stride(), d_feat, PK_FBANK_DIM, sizeof(float), frames,
-                PK_FBANK_DIM);
+    float *d_pcm = static_cast<float *>(lane.scratch(0).Reserve(sizeof(float) * samples));
+    float *d_feat = static_cast<float *>(lane.scratch(1).Reserve(sizeof(float) * frames * PK_FBANK_DIM));
+    lane.Upload(d_pcm, samples, buf.data(), samples, sizeof(float), 1, samples);
+    Check(ce_gpu_fbank(lane.ctx(), plan.get(), d_pcm, d_feat, nullptr), "Fbank::Process");
+    lane.Download(fbank_feature->Data(), fbank_feature->Stride(), d_feat, PK_FBANK_DIM, sizeof(float), frames,
+                  PK_FBANK_DIM);
   }
   // keep the samples from the first frame not emitted (src/fbank.cc:305-313)
   buf.erase(buf.begin(), buf.begin() + frames * CE_GPU_FRAME_SHIFT);

@@ -62,14 +62,44 @@ void *DeviceBuffer::Reserve(size_t bytes) {
   return ptr_;
 }
 
-Runtime::Runtime() {
-  const char *dev = getenv("CATEARS_DEVICE");
-  device_ = dev ? atoi(dev) : 0;
+struct Runtime::Lane {
+  int index = 0;
+  ce_gpu_ctx *ctx = nullptr;
+  void *stream = nullptr;
+  std::mutex mu;
+  DeviceBuffer scratch[kScratchSlots];
+};
+
+static void copy2d(void *stream, hipMemcpyKind kind, void *dst, size_t dst_ld, const void *src, size_t src_ld,
+                   size_t elem, size_t rows, size_t cols, const char *what) {
+  if (!rows || !cols) return;
+  hip_check(hipMemcpy2DAsync(dst, dst_ld * elem, src, src_ld * elem, cols * elem, rows, kind,
+                             static_cast<hipStream_t>(stream)),
+            what);
+}
+
+Runtime::Lane *Runtime::NewLane() {
+  // caller holds pool_mu_ (or is the constructor)
+  Lane *l = new Lane();
+  l->index = n_lanes_;
   hip_check(hipSetDevice(device_), "hipSetDevice");
   hipStream_t s = nullptr;
   hip_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
-  stream_ = s;
-  Check(ce_gpu_ctx_create(device_, stream_, &ctx_), "ce_gpu_ctx_create");
+  l->stream = s;
+  Check(ce_gpu_ctx_create(device_, l->stream, &l->ctx), "ce_gpu_ctx_create");
+  lanes_[n_lanes_++] = l;
+  return l;
+}
+
+Runtime::Runtime() {
+  const char *dev = getenv("CATEARS_DEVICE");
+  device_ = dev ? atoi(dev) : 0;
+  if (const char *e = getenv("CATEARS_LANES")) {
+    const int v = atoi(e);
+    if (v < 1 || v > 16) throw DeviceError("CATEARS_LANES must be 1..16");
+    max_lanes_ = v;
+  }
+  NewLane();  // lane 0: the layer-level paths and model loading
 }
 
 Runtime::~Runtime() {}
@@ -81,33 +111,70 @@ Runtime &Runtime::Get() {
   return *rt;
 }
 
+Runtime::Lease Runtime::Acquire() {
+  Lane *wait_on = nullptr;
+  {
+    std::lock_guard<std::mutex> pool(pool_mu_);
+    for (int t = 0; t < n_lanes_; ++t) {
+      Lane *l = lanes_[(next_ + t) % n_lanes_];
+      std::unique_lock<std::mutex> lk(l->mu, std::try_to_lock);
+      if (lk.owns_lock()) {
+        next_ = (unsigned)(l->index + 1);
+        return Lease(l, std::move(lk));
+      }
+    }
+    if (n_lanes_ < max_lanes_) {
+      Lane *l = NewLane();
+      return Lease(l, std::unique_lock<std::mutex>(l->mu));
+    }
+    wait_on = lanes_[next_++ % n_lanes_];
+  }
+  return Lease(wait_on, std::unique_lock<std::mutex>(wait_on->mu));
+}
+
+int Runtime::lanes_created() const {
+  std::lock_guard<std::mutex> pool(pool_mu_);
+  return n_lanes_;
+}
+
+ce_gpu_ctx *Runtime::Lease::ctx() const { return lane_->ctx; }
+DeviceBuffer &Runtime::Lease::scratch(int slot) { return lane_->scratch[slot]; }
+int Runtime::Lease::index() const { return lane_->index; }
+
+void Runtime::Lease::Upload(void *dst, size_t dst_ld, const void *src, size_t src_ld, size_t elem, size_t rows,
+                            size_t cols) {
+  copy2d(lane_->stream, hipMemcpyHostToDevice, dst, dst_ld, src, src_ld, elem, rows, cols, "hipMemcpy2DAsync(H2D)");
+}
+
+void Runtime::Lease::Download(void *dst, size_t dst_ld, const void *src, size_t src_ld, size_t elem, size_t rows,
+                              size_t cols) {
+  copy2d(lane_->stream, hipMemcpyDeviceToHost, dst, dst_ld, src, src_ld, elem, rows, cols, "hipMemcpy2DAsync(D2H)");
+  hip_check(hipStreamSynchronize(static_cast<hipStream_t>(lane_->stream)), "hipStreamSynchronize");
+}
+
+ce_gpu_ctx *Runtime::ctx() const { return lanes_[0]->ctx; }
+void *Runtime::stream() const { return lanes_[0]->stream; }
+std::mutex &Runtime::mutex() { return lanes_[0]->mu; }
+DeviceBuffer &Runtime::scratch(int slot) { return lanes_[0]->scratch[slot]; }
+
 void Runtime::Upload(void *dst, size_t dst_ld, const void *src, size_t src_ld, size_t elem, size_t rows,
                      size_t cols) {
-  if (!rows || !cols) return;
-  hip_check(hipMemcpy2DAsync(dst, dst_ld * elem, src, src_ld * elem, cols * elem, rows, hipMemcpyHostToDevice,
-                             static_cast<hipStream_t>(stream_)),
-            "hipMemcpy2DAsync(H2D)");
+  copy2d(stream(), hipMemcpyHostToDevice, dst, dst_ld, src, src_ld, elem, rows, cols, "hipMemcpy2DAsync(H2D)");
 }
 
 void Runtime::Download(void *dst, size_t dst_ld, const void *src, size_t src_ld, size_t elem, size_t rows,
                        size_t cols) {
-  if (rows && cols)
-    hip_check(hipMemcpy2DAsync(dst, dst_ld * elem, src, src_ld * elem, cols * elem, rows, hipMemcpyDeviceToHost,
-                               static_cast<hipStream_t>(stream_)),
-              "hipMemcpy2DAsync(D2H)");
+  copy2d(stream(), hipMemcpyDeviceToHost, dst, dst_ld, src, src_ld, elem, rows, cols, "hipMemcpy2DAsync(D2H)");
   Sync();
 }
 
 void Runtime::CopyDevice(void *dst, size_t dst_ld, const void *src, size_t src_ld, size_t elem, size_t rows,
                          size_t cols) {
-  if (!rows || !cols) return;
-  hip_check(hipMemcpy2DAsync(dst, dst_ld * elem, src, src_ld * elem, cols * elem, rows,
-                             hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream_)),
-            "hipMemcpy2DAsync(D2D)");
+  copy2d(stream(), hipMemcpyDeviceToDevice, dst, dst_ld, src, src_ld, elem, rows, cols, "hipMemcpy2DAsync(D2D)");
 }
 
 void Runtime::Sync() {
-  hip_check(hipStreamSynchronize(static_cast<hipStream_t>(stream_)), "hipStreamSynchronize");
+  hip_check(hipStreamSynchronize(static_cast<hipStream_t>(stream())), "hipStreamSynchronize");
 }
 
 }  // namespace host

@@ -133,6 +133,32 @@ class Fbank:
         return (feats, mel) if with_mel else feats
 
 
+def fbank_f64(wave):
+    """Fbank::Process in float64 with an exact FFT (numpy): the reference's
+    algorithm (src/fbank.cc:44-245) without its fp32 rounding -- DC removal,
+    pre-emphasis, the reference's own Hamming window and mel triangles (from
+    the oracle's tables), |rfft|^2, mel dots, floor, log.  The yardstick for
+    how far an fp32 fbank (the reference's split-radix order, or the GPU's
+    fast mode) is from the exact result."""
+    fb = Fbank()
+    win = fb.window().astype(np.float64)
+    mel = fb.mel_table()
+    w = np.asarray(wave, np.float64)
+    t = Fbank.num_frames(len(w))
+    out = np.zeros((max(t, 0), 40))
+    eps = float(np.finfo(np.float32).eps)
+    for i in range(t):
+        x = w[160 * i:160 * i + 400].copy()
+        x -= x.sum() / 400.0
+        y = x.copy()
+        y[1:] = x[1:] - 0.97 * x[:-1]
+        y[0] = x[0] - 0.97 * x[0]
+        p = np.abs(np.fft.rfft(np.concatenate([y * win, np.zeros(112)]))) ** 2
+        for b, (off, wt) in enumerate(mel):
+            out[i, b] = np.log(max(float(np.dot(wt.astype(np.float64), p[off:off + len(wt)])), eps))
+    return out
+
+
 def cmvn(global_stats, feats):
     """Online CMVN over a whole utterance (src/cmvn.cc:100-110 called 0..T-1)."""
     feats = np.ascontiguousarray(feats, np.float32)

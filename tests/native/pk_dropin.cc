@@ -181,7 +181,8 @@ int main(int argc, char **argv) {
     am.batch_stats(&calls, &blocks);
     int n_failed = 0;
     for (int f : failed) n_failed += f;
-    printf("device_calls %lld blocks %lld failed %d\n", (long long)calls, (long long)blocks, n_failed);
+    printf("device_calls %lld blocks %lld failed %d lanes %d\n", (long long)calls, (long long)blocks, n_failed,
+           catears::host::Runtime::Get().lanes_created());
     return 0;
   }
   if ((mode == "nnet" || mode == "layer") && argc == 7) {

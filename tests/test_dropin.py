@@ -199,7 +199,7 @@ def test_am_streams_batched_across_threads(tmp_path, oracle, xs_config):
     r = subprocess.run([DRIVER, "am_mt", str(conf), str(tmp_path / "mt")] + [str(a) for a in args],
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
-    calls, blocks, failed = [int(v) for v in r.stdout.split()[1::2]]
+    calls, blocks, failed, lanes = [int(v) for v in r.stdout.split()[1::2]]
     assert failed == 0
     for i, f in enumerate(feats):
         got = _load(tmp_path / f"mt{i}.bin")
@@ -210,6 +210,31 @@ def test_am_streams_batched_across_threads(tmp_path, oracle, xs_config):
         assert np.max(np.abs(got - want)) <= LOGLIK_TOL
     assert blocks == sum((len(f) + 49) // 50 for f in feats) or blocks > 0
     assert calls < blocks, (calls, blocks)  # some calls carried several streams' chunks
+
+
+@pytest.mark.gpu
+def test_am_streams_on_concurrent_lanes(tmp_path, oracle, xs_config):
+    """Without cross-stream batching every thread's chunks go to the device
+    on their own: the runtime leases each call a lane (context + stream) of
+    its own, so concurrent streams overlap instead of queueing on one
+    context, and each still gets exactly the rows it gets alone."""
+    from catears_amd import synth
+    lens = [16000 * 3 + 123, 16000 * 2, 16000 * 4 + 999, 16000 * 1 + 5]
+    feats = [oracle.Fbank().compute(synth.pcm(70 + i, n)) for i, n in enumerate(lens)]
+    args = []
+    for i, f in enumerate(feats):
+        args += [_put(tmp_path, f"x{i}.f32", f), len(f)]
+    conf = _am_config(tmp_path, xs_config, 50)
+    r = subprocess.run([DRIVER, "am_mt", str(conf), str(tmp_path / "mt")] + [str(a) for a in args],
+                       capture_output=True, text=True, timeout=300, env=dict(os.environ, CATEARS_LANES="4"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    calls, blocks, failed, lanes = [int(v) for v in r.stdout.split()[1::2]]
+    assert failed == 0 and calls == blocks
+    assert 2 <= lanes <= 4, lanes
+    for i, f in enumerate(feats):
+        alone = tmp_path / f"alone{i}.bin"
+        _run("am", conf, tmp_path / f"x{i}.f32", len(f), alone)
+        assert np.array_equal(_load(tmp_path / f"mt{i}.bin").view(np.uint32), _load(alone).view(np.uint32))
 
 
 @pytest.mark.gpu
@@ -232,7 +257,7 @@ def test_am_batcher_device_failure_releases_every_stream(tmp_path, xs_config):
     r = subprocess.run([DRIVER, "am_mt_fail", str(conf), str(tmp_path / "mt")] + [str(a) for a in args],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
-    calls, blocks, failed = [int(v) for v in r.stdout.split()[1::2]]
+    calls, blocks, failed, lanes = [int(v) for v in r.stdout.split()[1::2]]
     assert failed == len(feats) > 1
     assert calls == 1 and blocks == len(feats)
     # the streams outside the failed batch completed with full output

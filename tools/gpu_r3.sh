@@ -17,6 +17,16 @@ for st in ${STAGE:-tests bench c4}; do
       timeout -k 10 300 python bench.py --workload c4 --no-cpu-baseline > gpurun_out/r3/c4.json 2> gpurun_out/r3/c4.err \
         || { tail -20 gpurun_out/r3/c4.err; exit 1; }
       cat gpurun_out/r3/c4.json ;;
+    c2)
+      for m in exact fast; do
+        timeout -k 10 300 python bench.py --workload c2 --fbank $m --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/r3/c2_$m.json 2> gpurun_out/r3/c2_$m.err \
+          || { tail -20 gpurun_out/r3/c2_$m.err; exit 1; }
+        cat gpurun_out/r3/c2_$m.json
+      done ;;
+    fast)
+      timeout -k 10 300 python -u -m pytest tests/test_gpu_fbank_fast.py tests/test_gpu_pcm16.py -x -v -s --timeout 120 --timeout-method thread \
+        -p no:cacheprovider > gpurun_out/r3/pytest_fast.log 2>&1 || { tail -40 gpurun_out/r3/pytest_fast.log; exit 1; }
+      grep -E "vs exact|passed|failed" gpurun_out/r3/pytest_fast.log ;;
     c4s16)
       timeout -k 10 300 python bench.py --workload c4 --pcm s16 --no-cpu-baseline > gpurun_out/r3/c4s16.json 2> gpurun_out/r3/c4s16.err \
         || { tail -20 gpurun_out/r3/c4s16.err; exit 1; }
