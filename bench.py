@@ -168,7 +168,8 @@ def cpu_baseline(conf, n_utts, seconds, threads, min_wall):
 ROOFLINE_KERNEL = "gemm_f32_glds_kernel<catears::Cfg<128, 64, 32, 2, 2>, 2, false>"
 # split-plane hidden layers (split output), the default variants
 SPLIT_ROOFLINE_KERNEL = {
-    "bf16x6": "gemm_bf16x6f_kernel<catears::X6Cfg<128, 256, 2, 4, 2>, 8, 0, false>",
+    "bf16x6": "gemm_bf16x6d_kernel<catears::X6Cfg<256, 128, 4, 2, 2> >",  # CATEARS_X6_VARIANT 0 = 300
+    "bf16x6_160": "gemm_bf16x6f_kernel<catears::X6Cfg<128, 256, 2, 4, 2>, 8, 0, false>",
     "bf16x6p": "gemm_bf16x6q_kernel<catears::X6Cfg<128, 128, 4, 2, 3>, true, 0>",
     "f16x3": "gemm_f16x3_kernel<catears::X3Cfg<128, 128, 2, 4, 2, 64>, true>",
 }
@@ -349,7 +350,7 @@ def main_c2(args):
     if iv:
         avg_ms = sum(b - a for a, b in iv) / len(iv)
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-        kname = "fbank_fast_kernel" if args.fbank == "fast" else "fbank_kernel"
+        kname = ("fbank_fast_kernel" if args.fbank == "fast" else "fbank_kernel") + ("<short>" if s16 else "<float>")
         traffic, src = pmc_traffic(kname, "c2")
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
@@ -835,7 +836,9 @@ def main():
             # kernel instantiation for every layer (CATEARS_X6_F32IN=0: the
             # plane-operand kernels, hidden layers in their split-output form)
             f32in = split == "bf16x6" and os.environ.get("CATEARS_X6_F32IN", "1") != "0"
-            kname = SPLIT_ROOFLINE_KERNEL[split if f32in or split != "bf16x6" else "bf16x6p"]
+            variant = os.environ.get("CATEARS_X6_VARIANT", "0")
+            kname = SPLIT_ROOFLINE_KERNEL[("bf16x6_160" if variant == "160" else "bf16x6") if f32in else
+                                          split if split != "bf16x6" else "bf16x6p"]
             traffic, src = pmc_traffic(kname)
             eb = 4 if f32in else {"bf16x6": 6, "bf16x6p": 6, "f16x3": 4}[split]
             roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1),
