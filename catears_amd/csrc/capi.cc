@@ -1137,7 +1137,7 @@ static bool x6_f32in() {
 }
 
 static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, int ldx, int rows,
-                         const int *row_map, const float **y, int *ldy) {
+                         const int *row_map, const float **y, int *ldy, bool defer_final) {
   int max_in = 0;
   for (const Step &st : m->steps) max_in = std::max(max_in, st.gemm.kpad);
   for (const Step &st : m->steps) max_in = std::max(max_in, (st.gemm.n + 31) / 32 * 32);
@@ -1145,44 +1145,19 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
   CE_TRY(ensure_workspace(ctx, 2 * blk + (size_t)rows * m->num_pdfs));
   float *buf[2] = {ctx->workspace.as<float>(), ctx->workspace.as<float>() + blk};
   float *out = ctx->workspace.as<float>() + 2 * blk;
-  // latency mode: split-K slices per layer depend on K only (so results do
-  // not depend on the row count); workspace for the partials and tickets
-  // K-slices per tile: >= 6 K-tiles each, at most 8, and about 64 blocks
-  // for a single 128-row tile block (a streaming chunk): wide layers need
-  // fewer slices.  A function of the layer's K and N only.
-  // (CATEARS_LAT_SLICES="min_ktiles,max_slices,target_blocks" overrides the
-  // rule for measurements)
-  static const int *rule = [] {
-    static int r[3] = {6, 8, 64};
-    if (const char *e = getenv("CATEARS_LAT_SLICES")) {
-      int v[3];
-      if (sscanf(e, "%d,%d,%d", &v[0], &v[1], &v[2]) != 3 || v[0] < 1 || v[1] < 1 || v[2] < 1) return (int *)nullptr;
-      r[0] = v[0], r[1] = v[1], r[2] = v[2];
-    }
-    return r;
-  }();
-  if (ctx->latency && !rule)
-    return fail(CE_GPU_EINVAL, std::string("CATEARS_LAT_SLICES=") + getenv("CATEARS_LAT_SLICES") +
-                                   ": expected three positive integers min_ktiles,max_slices,target_blocks");
-  auto slices = [](int kpad, int n) {
-    const int cols = (n + 127) / 128, kt = kpad / 32;
-    const int s = std::max(1, std::min(std::min(rule[1], kt / rule[0]), (rule[2] + cols - 1) / cols));
-    const int per = (kt + s - 1) / s;
-    return (kt + per - 1) / per;  // no empty slice
-  };
+  // latency mode (kernels/gemm_bf16x6_lat.hip): every layer's K split into
+  // x6_lat_slices(K, N) slices -- a function of the layer only, so results do
+  // not depend on the row count -- partials in ctx->split_part
   if (ctx->latency) {
-    size_t part = 0, tickets = 0;
+    size_t part = 0;
     for (size_t i = 0; i < m->steps.size(); ++i) {
       const GemmLayer &g = m->steps[i].gemm;
       const int kpad = i == 0 ? g.kpad : g.nseg * g.din;
-      part = std::max(part, x6_split_part_floats(rows, g.n, slices(kpad, g.n)));
-      tickets = std::max(tickets, x6_split_tiles(rows, g.n));
+      part = std::max(part, x6_lat_part_floats(rows, g.n, x6_lat_slices(kpad, g.n)));
     }
-    if (ctx->split_part.bytes < part * sizeof(float) || ctx->split_ticket.bytes < tickets * sizeof(unsigned)) {
-      CE_HIP(hipStreamSynchronize(ctx->stream));  // the old buffers may still be in use
+    if (ctx->split_part.bytes < part * sizeof(float)) {
+      CE_HIP(hipStreamSynchronize(ctx->stream));  // the old buffer may still be in use
       CE_TRY(ctx->split_part.alloc(part * sizeof(float)));
-      CE_TRY(ctx->split_ticket.alloc(tickets * sizeof(unsigned)));
-      CE_HIP(hipMemsetAsync(ctx->split_ticket.ptr, 0, tickets * sizeof(unsigned), ctx->stream));
     }
   }
   const float *xs = nullptr;
@@ -1192,7 +1167,17 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
     const GemmLayer &g = m->steps[i].gemm;
     const bool last = i + 1 == m->steps.size();
     X6Gemm a;
-    if (i == 0) {
+    // the latency kernel splices the caller's rows itself (din % 8 == 0)
+    const bool lat_direct = ctx->latency && i == 0 && g.din % 8 == 0 && ldx % 4 == 0 &&
+                            (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+    if (lat_direct) {
+      xs = x;
+      px = ldx;
+      a.din = g.din;
+      a.nseg = g.nseg;
+      for (int s = 0; s < 8; ++s) a.off[s] = g.off[s];
+      a.row_map = row_map;
+    } else if (i == 0) {
       ProfScope prof(ctx, CE_GPU_PROF_GEMM_GATHER);
       CE_TRY(launch_splice_pad(ctx->stream, x, ldx, rows, g.din, g.nseg, g.off, row_map, buf[cur], g.kpad));
       xs = buf[cur];
@@ -1224,15 +1209,20 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
     const int pn = (g.n + 31) / 32 * 32;
     a.y32 = last ? out : buf[cur];
     a.ldy = last ? g.n : pn;
-    if (ctx->latency) {
-      a.splitk = slices(a.kpad, a.n);
-      a.part = ctx->split_part.as<float>();
-      a.ticket = ctx->split_ticket.as<unsigned>();
-      a.split_tiles = ctx->split_ticket.bytes / sizeof(unsigned);
-    }
     {
       ProfScope prof(ctx, CE_GPU_PROF_GEMM);
-      CE_TRY(launch_gemm_bf16x6(ctx->stream, a));
+      if (ctx->latency) {
+        // the last layer's reduce fused into the finalize launch
+        const bool defer = last && defer_final && rows <= kX6LatWindow;
+        CE_TRY(launch_gemm_bf16x6_lat(ctx->stream, a, ctx->split_part.as<float>(),
+                                      ctx->split_part.bytes / sizeof(float), !defer));
+        if (defer) {
+          ctx->lat_pending = true;
+          ctx->lat_last = a;
+        }
+      } else {
+        CE_TRY(launch_gemm_bf16x6(ctx->stream, a));
+      }
     }
     xs = buf[cur];
     px = pn;
@@ -1444,15 +1434,32 @@ static int run_steps_i8(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, 
   return CE_GPU_OK;
 }
 
+// defer_final: the caller hands y to finalize_output only, so a latency-mode
+// last layer may leave its reduce to that launch (ctx->lat_pending)
 static int run_steps(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, int ldx, int rows,
-                     const int *row_map, const uint32_t *row_edge, const float **y, int *ldy) {
+                     const int *row_map, const uint32_t *row_edge, const float **y, int *ldy,
+                     bool defer_final = false) {
+  ctx->lat_pending = false;
   if (m->int8) return run_steps_i8(ctx, m, x, ldx, rows, row_map, row_edge, y, ldy);
   if (m->gemm == CE_GPU_GEMM_F16X3) return run_steps_x3(ctx, m, x, ldx, rows, row_map, y, ldy);
   if (m->gemm == CE_GPU_GEMM_BF16X6_PLANES) return run_steps_x6(ctx, m, x, ldx, rows, row_map, y, ldy);
   if (m->gemm == CE_GPU_GEMM_BF16X6)
-    return x6_f32in() ? run_steps_x6f(ctx, m, x, ldx, rows, row_map, y, ldy)
+    return x6_f32in() ? run_steps_x6f(ctx, m, x, ldx, rows, row_map, y, ldy, defer_final)
                       : run_steps_x6(ctx, m, x, ldx, rows, row_map, y, ldy);
   return run_steps_f32(ctx, m, x, ldx, rows, row_map, y, ldy);
+}
+
+// launch_finalize on rows first .. first + rows - 1 of run_steps' output, or
+// the fused reduce + finalize when run_steps left the last reduce pending
+static int finalize_output(ce_gpu_ctx *ctx, const float *y, int ldy, int first, int rows, int dim,
+                           bool log_softmax, const float *log_prior, const int *row_dst, float *out) {
+  if (ctx->lat_pending) {
+    ctx->lat_pending = false;
+    return launch_lat_finalize(ctx->stream, ctx->lat_last, ctx->split_part.as<float>(), first, rows, log_softmax,
+                               log_prior, row_dst, out);
+  }
+  return launch_finalize(ctx->stream, y + (size_t)first * ldy, ldy, rows, dim, log_softmax, log_prior, row_dst,
+                         out);
 }
 
 // Quantize (src/matrix.cc:329-387) of one weight matrix on the host at load
@@ -1531,10 +1538,10 @@ int ce_gpu_am_forward(ce_gpu_ctx *ctx, const ce_gpu_model *m, const ce_gpu_plan 
     const float *y = nullptr;
     int ldy = 0;
     const uint32_t *row_edge = p->d_row_edge.as<uint32_t>() + c.map_base;
-    CE_TRY(run_steps(ctx, m, d_feats, m->input_dim, c.rows, row_src, row_edge, &y, &ldy));
+    CE_TRY(run_steps(ctx, m, d_feats, m->input_dim, c.rows, row_src, row_edge, &y, &ldy, true));
     ProfScope prof(ctx, CE_GPU_PROF_FINALIZE);
-    CE_TRY(launch_finalize(ctx->stream, y, ldy, c.rows, m->num_pdfs, m->final_log_softmax,
-                           m->log_prior.as<float>(), row_dst, d_loglik));
+    CE_TRY(finalize_output(ctx, y, ldy, 0, c.rows, m->num_pdfs, m->final_log_softmax, m->log_prior.as<float>(),
+                           row_dst, d_loglik));
   }
   return CE_GPU_OK;
 }
@@ -1580,11 +1587,10 @@ int ce_gpu_nnet_propagate(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *d
   }
   const float *y = nullptr;
   int ldy = 0;
-  CE_TRY(run_steps(ctx, m, d_in, ld_in, rows, nullptr, nullptr, &y, &ldy));
+  CE_TRY(run_steps(ctx, m, d_in, ld_in, rows, nullptr, nullptr, &y, &ldy, true));
   ProfScope prof(ctx, CE_GPU_PROF_FINALIZE);
-  return launch_finalize(ctx->stream, y + (size_t)m->net_left * ldy, ldy, out_rows, m->num_pdfs,
-                         m->final_log_softmax, subtract_prior ? m->log_prior.as<float>() : nullptr, nullptr,
-                         d_out);
+  return finalize_output(ctx, y, ldy, m->net_left, out_rows, m->num_pdfs, m->final_log_softmax,
+                         subtract_prior ? m->log_prior.as<float>() : nullptr, nullptr, d_out);
 }
 
 int ce_gpu_nnet_propagate_blocks(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *d_in, int ld_in,
@@ -1638,9 +1644,9 @@ int ce_gpu_nnet_propagate_blocks(ce_gpu_ctx *ctx, const ce_gpu_model *m, const f
   int ldy = 0;
   // blocks are independent: the rows a Splice reads across a block boundary
   // only feed rows that block's Narrow drops
-  CE_TRY(run_steps(ctx, m, d_in, ld_in, rows, nullptr, d_edge, &y, &ldy));
+  CE_TRY(run_steps(ctx, m, d_in, ld_in, rows, nullptr, d_edge, &y, &ldy, true));
   ProfScope prof(ctx, CE_GPU_PROF_FINALIZE);
-  return launch_finalize(ctx->stream, y, ldy, rows, m->num_pdfs, m->final_log_softmax,
+  return finalize_output(ctx, y, ldy, 0, rows, m->num_pdfs, m->final_log_softmax,
                          subtract_prior ? m->log_prior.as<float>() : nullptr, d_dst, d_out);
 }
 

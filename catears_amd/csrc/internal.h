@@ -146,6 +146,24 @@ __device__ __forceinline__ float apply_post(float y, float sc, float of, const i
   return y;
 }
 
+// The latency GEMM's split-K reduce (kernels/gemm_bf16x6_lat.hip): the S
+// partials of 4 consecutive outputs at src + s * stride, summed in slice
+// order with sixteen loads in flight.
+__device__ __forceinline__ float4 lat_slice_sum(const float *src, size_t stride, int slices) {
+  float4 sum = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  for (int s0 = 0; s0 < slices; s0 += 16) {
+    float4 v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (s0 + u < slices) v[u] = *reinterpret_cast<const float4 *>(src + (size_t)(s0 + u) * stride);
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (s0 + u < slices)
+        sum = s0 + u == 0 ? v[u] : make_float4(sum.x + v[u].x, sum.y + v[u].y, sum.z + v[u].z, sum.w + v[u].w);
+  }
+  return sum;
+}
+
 // Calls f(std::integral_constant<int, MODE>) for the runtime mode.
 template <class F>
 __device__ __forceinline__ void with_post_mode(int mode, F &&f) {
@@ -216,6 +234,36 @@ struct Step {
   RowOp row;
 };
 
+// One bf16x6 GEMM launch (kernels/gemm_bf16x6*.hip).
+struct X6Gemm {
+  const uint16_t *x = nullptr;
+  int ldx = 0, px = 0;
+  const uint16_t *w = nullptr;
+  int ldw = 0, pw = 0;
+  // fp32 operands instead (xf rows x ldx floats, wf n x ldw floats, both
+  // K-contiguous): split into the three planes on the way into LDS; the
+  // output is then fp32 (y32) for every layer
+  const float *xf = nullptr, *wf = nullptr;
+  // the same weights as MFMA A fragments (gemm_bf16x6d_kernel, the default
+  // with fp32 activations): for 16-unit block u, K-tile t (32 k) and plane p
+  // the 1 KB at ((u * wd_kt + t) * 3 + p) * 512 elements holds lane l's 8
+  // bf16 (unit 16 u + (l & 15), k = 32 t + 8 (l >> 4) ..+7) at 8 l; units
+  // zero-padded to a multiple of kX6DirUnits
+  const uint16_t *wd = nullptr;
+  int wd_kt = 0;
+  int m = 0, n = 0, kpad = 0, din = 0, nseg = 1;
+  int off[8] = {0};
+  // latency kernel only: input row r of segment s is xf row
+  // row_map[clamp(r + off[s])] (the first layer reading the caller's rows)
+  const int *row_map = nullptr;
+  const float *bias = nullptr, *bn_scale = nullptr, *bn_offset = nullptr;
+  int post[4] = {0, 0, 0, 0};
+  int npost = 0;
+  float *y32 = nullptr;
+  uint16_t *y16 = nullptr;
+  int ldy = 0, py = 0;
+};
+
 }  // namespace catears
 
 // ------------------------------------------------------------ ABI objects --
@@ -232,8 +280,11 @@ struct ce_gpu_ctx {
   catears::DevBuf overflow;    // int: an f16x3 split left the fp16 range (ce_gpu_ctx_overflow)
   int latency = 0;             // ce_gpu_ctx_set_latency: split-K GEMMs for small batches
   int fbank_mode = 0;          // ce_gpu_ctx_set_fbank: CE_GPU_FBANK_EXACT / _FAST
-  catears::DevBuf split_part;  // latency mode: GEMM partials (grown on demand)
-  catears::DevBuf split_ticket;  // latency mode: per-tile arrival counters (zeroed when grown)
+  catears::DevBuf split_part;  // latency mode: GEMM slice partials (grown on demand)
+  // latency mode: the last layer's slice reduce left to the finalize launch
+  // (run_steps with defer_final; consumed by finalize_output in capi.cc)
+  bool lat_pending = false;
+  catears::X6Gemm lat_last;
   std::vector<int32_t> h_blk_maps;
   // optional per-class launch timing (ce_gpu_ctx_profile)
   bool profiling = false;
@@ -354,45 +405,25 @@ int gemm_k_align();
 // stride px, read through the splice offsets (K-tile of 32 inside one
 // segment); w: n x ldw, plane stride pw (zero padded to kpad); output split
 // (y16, plane stride py) or fp32 (y32).
-struct X6Gemm {
-  const uint16_t *x = nullptr;
-  int ldx = 0, px = 0;
-  const uint16_t *w = nullptr;
-  int ldw = 0, pw = 0;
-  // fp32 operands instead (xf rows x ldx floats, wf n x ldw floats, both
-  // K-contiguous): split into the three planes on the way into LDS; the
-  // output is then fp32 (y32) for every layer
-  const float *xf = nullptr, *wf = nullptr;
-  // the same weights as MFMA A fragments (gemm_bf16x6d_kernel, the default
-  // with fp32 activations): for 16-unit block u, K-tile t (32 k) and plane p
-  // the 1 KB at ((u * wd_kt + t) * 3 + p) * 512 elements holds lane l's 8
-  // bf16 (unit 16 u + (l & 15), k = 32 t + 8 (l >> 4) ..+7) at 8 l; units
-  // zero-padded to a multiple of kX6DirUnits
-  const uint16_t *wd = nullptr;
-  int wd_kt = 0;
-  int m = 0, n = 0, kpad = 0, din = 0, nseg = 1;
-  int off[8] = {0};
-  const float *bias = nullptr, *bn_scale = nullptr, *bn_offset = nullptr;
-  int post[4] = {0, 0, 0, 0};
-  int npost = 0;
-  float *y32 = nullptr;
-  uint16_t *y16 = nullptr;
-  int ldy = 0, py = 0;
-  // latency mode (fp32 operands): K split over `splitk` blocks per output
-  // tile, partials in `part` (x6_split_part_floats), one zeroed ticket per
-  // tile (at least x6_split_tiles); the sum over slices is in slice order
-  int splitk = 1;
-  float *part = nullptr;
-  unsigned *ticket = nullptr;
-  size_t split_tiles = 0;
-};
 int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a);
 constexpr int kX6DirUnits = 256;  // gemm_bf16x6d_kernel's unit tile
-size_t x6_split_part_floats(int m, int n, int splitk);
-size_t x6_split_tiles(int m, int n);
-// latency-mode GEMMs run in launches of at most this many rows (bounds the
-// partial workspace: <= 16 x 27 tiles x 8 slices x 64 KB)
-constexpr int kX6SplitWindow = 2048;
+// Latency mode v2 (kernels/gemm_bf16x6_lat.hip): K split into
+// x6_lat_slices(kpad, n) slices (a function of K and N only), every slice's
+// fp32 partial stored, then summed in slice order by a reduce kernel that
+// applies bias / ReLU / BatchNorm; needs the weight fragment image (a.wd) and
+// fp32 activations (din a multiple of 8: a segment may end inside a K-tile).
+// part: x6_lat_part_floats(rows, n, slices) floats.  reduce = false (rows <=
+// kX6LatWindow) leaves the partials for launch_lat_finalize.
+constexpr int kX6LatWindow = 1024;
+int x6_lat_slices(int kpad, int n);
+size_t x6_lat_part_floats(int rows, int n, int slices);
+int launch_gemm_bf16x6_lat(hipStream_t s, const X6Gemm &a, float *part, size_t part_floats, bool reduce = true);
+// The last layer's slice reduce fused with launch_finalize: rows first ..
+// first + rows - 1 of the a.m-row partials of a (launch_gemm_bf16x6_lat with
+// reduce = false) summed, + bias, post chain, then (log-softmax) - prior into
+// out (row_dst as launch_finalize) -- the bits of reduce then finalize.
+int launch_lat_finalize(hipStream_t s, const X6Gemm &a, const float *part, int first, int rows, bool log_softmax,
+                        const float *log_prior, const int *row_dst, float *out);
 // splice_pad (below) written as three bf16 planes of width po: out row r at
 // out + r * 3 * po.
 int launch_splice_pad_split(hipStream_t s, const float *in, int ld_in, int rows, int din, int nseg, const int *off,

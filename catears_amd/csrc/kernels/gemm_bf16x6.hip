@@ -68,10 +68,6 @@ struct X6Args {
   int post[4];
   int npost, post_mode;
   int tiles_m, tiles_n, group;
-  float *part;       // split-K (latency mode): fp32 partials, splitk per tile
-  unsigned *ticket;  // split-K: arrival counter per tile, zero between launches
-  int splitk;
-  int row0;          // split-K: first row of this launch's row window
   const uint16_t *wd;  // weights as MFMA A fragments (gemm_bf16x6d_kernel), see X6Gemm::wd
   int wd_kt;           // K-tiles per 16-unit block in that image
 };
@@ -359,12 +355,9 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6q_kernel(X6Args p) {
 // 2 = no global loads after the prologue, 4 = no MFMAs, 8 = no fragment
 // reads after the first tile, 16 = no K-tile barrier, 32 = no plane writes
 // after the prologue.
-// SPLIT (latency mode, SCHED 0 only): the K-tiles are split over p.splitk
-// blocks per output tile (see the fix-up after the loop).
-template <class C, int SCHED, int DIAG = 0, bool SPLIT = false>
+template <class C, int SCHED, int DIAG = 0>
 __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
   constexpr int BW = C::BW, BF = C::BF, TW = C::TW, TF = C::TF, NT = C::NT, STAGE = C::STAGE;
-  static_assert(!SPLIT || SCHED == 0, "split-K runs in the SCHED 0 loop");
 #ifndef CATEARS_DIAG
   static_assert(DIAG == 0, "ablation builds (wrong results) only with -DCATEARS_DIAG");
 #endif
@@ -378,32 +371,16 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ww = wave / C::WGF, wf = wave % C::WGF;
-  // split-K: block b = 8 S q + 8 h + r computes K-slice h of tile 8 q + r
-  // (the slices of a tile share an XCD under round-robin dispatch: speed
-  // only); the grid is padded to whole groups of 8 S blocks
-  int tile = blockIdx.x, slice = 0, row0 = 0;
-  if constexpr (SPLIT) {
-    const int g = 8 * p.splitk, rem = blockIdx.x % g;
-    slice = rem >> 3;
-    tile = (blockIdx.x / g) * 8 + (rem & 7);
-    row0 = p.row0;  // this launch's row window (tiles_m covers the window only)
-    if (tile >= p.tiles_m * p.tiles_n) return;
-  }
   int tm, tn;
-  tile_of(tile, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
-  const int f0 = row0 + tm * BF, n0 = tn * BW;
+  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
+  const int f0 = tm * BF, n0 = tn * BW;
   const int prow = tid >> 2, pch = tid & 3;
 
   typedef const __attribute__((address_space(1))) f32x4v gvec;
   uint32_t wsrc[NPW];  // float offset of this thread's weight row at k = 0
 #pragma unroll
   for (int i = 0; i < NPW; ++i) wsrc[i] = (uint32_t)(min(n0 + prow + i * RPP, p.n - 1) * p.ldw + 8 * pch);
-  int kbeg = 0, ktiles = p.kpad / 32;  // this block's K-tiles: kbeg .. ktiles-1
-  if constexpr (SPLIT) {
-    const int per = (ktiles + p.splitk - 1) / p.splitk;
-    kbeg = min(slice * per, ktiles);
-    ktiles = min(kbeg + per, ktiles);
-  }
+  const int kbeg = 0, ktiles = p.kpad / 32;
   f32x4v rw0[NPW], rw1[NPW], rx0[NPX], rx1[NPX];
   auto load = [&](int kt) {
     if constexpr ((DIAG & 2) != 0) {
@@ -649,75 +626,6 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
     __builtin_amdgcn_s_barrier();
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if constexpr (SPLIT) {
-    // Last-arriver fix-up (MI355X_MICROARCH.md, inter-workgroup hand-offs,
-    // the table's first row, one block per CU): every slice publishes its
-    // fp32 partial in the accumulator layout with 8-B agent-scope stores
-    // (write-through, sc1), each wave drains them (vmcnt(0)), the block
-    // barrier, then one agent-scope add on the tile's ticket; the block whose
-    // add returns S-1 reads the other slices' partials with 8-B agent-scope
-    // loads and sums all S in slice order -- the same value whichever slice
-    // arrives last -- and runs the epilogue; the others exit.  No release
-    // fence (it would write back the XCD's dirty L2); the winner acquires.
-    // No wave ever waits on another block.
-    constexpr int WF4 = TW * TF * 64;  // f32x4 per wave and slice
-    typedef unsigned long long u64;
-    u64 *base = reinterpret_cast<u64 *>(p.part) + 2 * ((size_t)tile * p.splitk * C::NW * WF4 + wave * WF4 + lane);
-    const size_t sstride = 2 * (size_t)C::NW * WF4;  // u64 per slice
-#pragma unroll
-    for (int i = 0; i < TW; ++i)
-#pragma unroll
-      for (int j = 0; j < TF; ++j) {
-        u64 *d = base + slice * sstride + 2 * 64 * (i * TF + j);
-        const f32x4 v = acc[i][j];
-        __hip_atomic_store(d, __builtin_bit_cast(u64, (f32x2t{v[0], v[1]})), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(d + 1, __builtin_bit_cast(u64, (f32x2t{v[2], v[3]})), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __shared__ unsigned s_arrived;
-    __syncthreads();
-    if (tid == 0) {
-      s_arrived = __hip_atomic_fetch_add(p.ticket + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // The last arriver acquires at agent scope before any wave of its
-      // block reads the other slices' partials (buffer_inv sc1 of this CU's
-      // L1, then the wait for it, then the barrier that releases the other
-      // waves).  The partial loads below are sc1 besides, so the hand-off is
-      // ordered by the language's acquire and not only by the ISA's L1
-      // bypass.  The store side needs no release fence: each slice's partials
-      // are sc1 (write-through) stores, drained by every storing wave's
-      // vmcnt(0) before the block barrier that precedes the ticket add --
-      // they have left this XCD's L2 before the add can be seen
-      // (MI355X_MICROARCH.md, hand-off table, first row).  A release here
-      // would write back the XCD's whole dirty L2 per block (the 30 % loss
-      // DESIGN.md §8 records).
-      if (s_arrived == (unsigned)p.splitk - 1) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    }
-    __syncthreads();
-    if (s_arrived != (unsigned)p.splitk - 1) return;
-    if (tid == 0) __hip_atomic_store(p.ticket + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
-    f32x4 sum[TW][TF];
-    for (int h = 0; h < p.splitk; ++h) {
-#pragma unroll
-      for (int i = 0; i < TW; ++i)
-#pragma unroll
-        for (int j = 0; j < TF; ++j) {
-          f32x4 v = acc[i][j];
-          if (h != slice) {
-            const u64 *src = base + h * sstride + 2 * 64 * (i * TF + j);
-            const f32x2t lo = __builtin_bit_cast(f32x2t, __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            const f32x2t hi = __builtin_bit_cast(f32x2t, __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            v = f32x4{lo[0], lo[1], hi[0], hi[1]};
-          }
-          sum[i][j] = h == 0 ? v : sum[i][j] + v;
-        }
-    }
-    x6_epilogue<TW, TF, false>(p, sum, n0 + wrow, f0 + frow, lane);
-    return;
-  }
-
   x6_epilogue<TW, TF, false>(p, acc, n0 + wrow, f0 + frow, lane);
 }
 
@@ -1095,44 +1003,6 @@ int launch_ws(hipStream_t s, X6Args p) {
   return CE_GPU_OK;
 }
 
-// Latency mode: split-K over a.splitk blocks per tile (a.part / a.ticket
-// from the caller's workspace, sized by x6_split_part_floats /
-// x6_split_tiles).
-// One launch per window of kX6SplitWindow rows (whole tiles), so the
-// partial workspace stays bounded for long blocks; tiles never straddle a
-// window, so the results do not depend on the windowing.
-template <class C, int PAD = 0>
-int launch_f_split(hipStream_t s, X6Args p, const X6Gemm &a) {
-  static_assert(kX6SplitWindow % C::BF == 0, "window of whole tiles");
-  // PAD: dynamic LDS that keeps the block alone on its CU (the write-through
-  // hand-off above is the measured one-block-per-CU form)
-  p.tiles_n = (p.n + C::BW - 1) / C::BW;
-  p.part = a.part;
-  p.ticket = a.ticket;
-  p.splitk = a.splitk;
-  for (int r0 = 0; r0 < p.m; r0 += kX6SplitWindow) {
-    p.row0 = r0;
-    p.tiles_m = (std::min(kX6SplitWindow, p.m - r0) + C::BF - 1) / C::BF;
-    const int tiles = p.tiles_m * p.tiles_n;
-    if ((size_t)tiles > a.split_tiles || !a.part || !a.ticket)
-      return fail(CE_GPU_EINVAL, "gemm_bf16x6: split-K workspace too small");
-    dim3 grid((tiles + 7) / 8 * 8 * a.splitk), block(C::NT);
-    hipLaunchKernelGGL((gemm_bf16x6f_kernel<C, 0, 0, true>), grid, block, PAD, s, p);
-    CE_HIP(hipGetLastError());
-  }
-  return CE_GPU_OK;
-}
-
-// latency-mode tiles: 128 units x 128 frames, 8 waves of 32 x 64; for row
-// blocks of at most kX6LatSmallRows (a streaming chunk) 128 x 64, 4 waves of
-// 64 x 32 (72 KB of LDS, padded to one block per CU).  The tile shape does
-// not change any output bit (same K-tile and product order per element,
-// slices by K and N only).
-typedef X6Cfg<128, 128, 4, 2, 2> X6LatCfg;
-typedef X6Cfg<128, 64, 2, 2, 2> X6LatSmallCfg;
-constexpr int kX6LatSmallRows = 256;
-constexpr int kX6LatSmallPad = 82 * 1024 - 2 * X6LatSmallCfg::STAGE;
-
 // CATEARS_X6_VARIANT: the schedule of the fp32-activation bf16x6 GEMM.
 // The product build carries the default (0 = 300, direct weights: 256 x 128
 // tiles, weight fragments straight from L2 to registers), the round-2
@@ -1205,16 +1075,9 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
   p.npost = a.npost;
   p.post_mode = post_mode(a.post, a.npost);
   p.group = 8;
-  p.part = nullptr;
-  p.ticket = nullptr;
-  p.splitk = 1;
-  p.row0 = 0;
   p.wd = a.wd;
   p.wd_kt = a.wd_kt;
   const bool out16 = a.y16 != nullptr;
-  if (f32in && a.splitk > 1)
-    return a.m <= kX6LatSmallRows ? launch_f_split<X6LatSmallCfg, kX6LatSmallPad>(s, p, a)
-                                  : launch_f_split<X6LatCfg>(s, p, a);
   if (f32in) {
     switch (x6_variant()) {
       case 0:
@@ -1272,24 +1135,6 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
   }
   // plane operands (CATEARS_X6_F32IN=0 / CE_GPU_GEMM_BF16X6_PLANES)
   return launch_q<X6Cfg<128, 128, 4, 2, 3>, 0>(s, p, out16);
-}
-
-size_t x6_split_tiles(int m, int n) {
-  m = std::min(m, kX6SplitWindow);
-  const size_t cols = (n + X6LatCfg::BW - 1) / X6LatCfg::BW;
-  const size_t big = (m + X6LatCfg::BF - 1) / X6LatCfg::BF * cols;
-  const size_t small = m <= kX6LatSmallRows ? (m + X6LatSmallCfg::BF - 1) / X6LatSmallCfg::BF * cols : 0;
-  return std::max(big, small);
-}
-
-size_t x6_split_part_floats(int m, int n, int splitk) {
-  m = std::min(m, kX6SplitWindow);
-  const size_t cols = (n + X6LatCfg::BW - 1) / X6LatCfg::BW;
-  const size_t big = (m + X6LatCfg::BF - 1) / X6LatCfg::BF * cols * X6LatCfg::BW * X6LatCfg::BF;
-  const size_t small = m <= kX6LatSmallRows
-                           ? (m + X6LatSmallCfg::BF - 1) / X6LatSmallCfg::BF * cols * X6LatSmallCfg::BW * X6LatSmallCfg::BF
-                           : 0;
-  return std::max(big, small) * splitk;
 }
 
 int launch_splice_pad_split(hipStream_t s, const float *in, int ld_in, int rows, int din, int nseg, const int *off,

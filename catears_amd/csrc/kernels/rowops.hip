@@ -70,17 +70,11 @@ __global__ __launch_bounds__(256) void finalize_kernel(const float *__restrict__
 // lane l holds float4 chunks l, l + 64, ... of its row.
 constexpr int kMaxVecPerLane = 16;  // rows up to 4096 wide
 
-template <bool LOGSM>
-__global__ __launch_bounds__(256) void finalize_vec_kernel(const float *__restrict__ x, int ldx, int rows, int dim,
-                                                           const float *__restrict__ prior,
-                                                           const int *__restrict__ row_dst,
-                                                           float *__restrict__ out) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (row >= rows) return;
-  const int dst = row_dst ? row_dst[row] : row;
-  if (dst < 0) return;
-  const float4 *xr = reinterpret_cast<const float4 *>(x + (int64_t)row * ldx);
-  float4 *o = reinterpret_cast<float4 *>(out + (int64_t)dst * dim);
+// One row: load(c) gives float4 chunk c of the row's values.
+template <bool LOGSM, class Load>
+__device__ __forceinline__ void finalize_row_vec(Load &&load, int dim, const float *__restrict__ prior, float *o_row,
+                                                 int lane) {
+  float4 *o = reinterpret_cast<float4 *>(o_row);
   const float4 *pr = reinterpret_cast<const float4 *>(prior);
   const int d4 = dim >> 2;
   float4 v[kMaxVecPerLane];
@@ -88,7 +82,7 @@ __global__ __launch_bounds__(256) void finalize_vec_kernel(const float *__restri
 #pragma unroll
   for (int j = 0; j < kMaxVecPerLane; ++j) {
     const int c = lane + 64 * j;
-    v[j] = c < d4 ? xr[c] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    v[j] = c < d4 ? load(c) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     if (LOGSM && c < d4) s += expf(v[j].x) + expf(v[j].y) + expf(v[j].z) + expf(v[j].w);
   }
   const float ls = LOGSM ? logf(wave_sum(s)) : 0.0f;
@@ -105,6 +99,64 @@ __global__ __launch_bounds__(256) void finalize_vec_kernel(const float *__restri
       o[c] = y;
     }
   }
+}
+
+template <bool LOGSM>
+__global__ __launch_bounds__(256) void finalize_vec_kernel(const float *__restrict__ x, int ldx, int rows, int dim,
+                                                           const float *__restrict__ prior,
+                                                           const int *__restrict__ row_dst,
+                                                           float *__restrict__ out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const int dst = row_dst ? row_dst[row] : row;
+  if (dst < 0) return;
+  const float4 *xr = reinterpret_cast<const float4 *>(x + (int64_t)row * ldx);
+  finalize_row_vec<LOGSM>([&](int c) { return xr[c]; }, dim, prior, out + (int64_t)dst * dim, lane);
+}
+
+// finalize_vec_kernel reading the last layer's latency-GEMM partials instead
+// of its output: per 4 outputs the slice sum, + bias, the post chain -- the
+// reduce kernel's arithmetic -- then the same row math.
+struct LatFinalizeArgs {
+  const float *part;
+  int slices, m, first, rows, dim;
+  const float *bias, *bn_scale, *bn_offset;
+  int post[4];
+  int npost;
+  const float *prior;
+  const int *row_dst;
+  float *out;
+};
+
+// One block per row: the 256 threads reduce the row's float4 chunks into LDS
+// (the slice loads of the whole row in flight together), then wave 0 runs the
+// finalize row math on them.
+template <bool LOGSM>
+__global__ __launch_bounds__(256) void lat_finalize_kernel(LatFinalizeArgs p) {
+  __shared__ float4 vals[64 * kMaxVecPerLane];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const int dst = p.row_dst ? p.row_dst[row] : row;
+  if (dst < 0) return;  // block-uniform
+  const float *src = p.part + (size_t)(p.first + row) * p.dim;
+  const size_t stride = (size_t)p.m * p.dim;
+  auto reduce = [&](int c) {
+    const float4 s4 = lat_slice_sum(src + 4 * c, stride, p.slices);
+    const float4 b = p.bias ? reinterpret_cast<const float4 *>(p.bias)[c] : make_float4(-0.0f, -0.0f, -0.0f, -0.0f);
+    float4 sc = make_float4(1.0f, 1.0f, 1.0f, 1.0f), of = make_float4(-0.0f, -0.0f, -0.0f, -0.0f);
+    if (p.npost) {
+      if (p.bn_scale) sc = reinterpret_cast<const float4 *>(p.bn_scale)[c];
+      if (p.bn_offset) of = reinterpret_cast<const float4 *>(p.bn_offset)[c];
+    }
+    return make_float4(apply_post<kPostModeGeneric>(s4.x + b.x, sc.x, of.x, p.post, p.npost),
+                       apply_post<kPostModeGeneric>(s4.y + b.y, sc.y, of.y, p.post, p.npost),
+                       apply_post<kPostModeGeneric>(s4.z + b.z, sc.z, of.z, p.post, p.npost),
+                       apply_post<kPostModeGeneric>(s4.w + b.w, sc.w, of.w, p.post, p.npost));
+  };
+  const int d4 = p.dim >> 2;
+  for (int c = tid; c < d4; c += 256) vals[c] = reduce(c);
+  __syncthreads();
+  if (tid >= 64) return;
+  finalize_row_vec<LOGSM>([&](int c) { return vals[c]; }, p.dim, p.prior, p.out + (int64_t)dst * p.dim, tid);
 }
 
 __global__ __launch_bounds__(256) void rowop_kernel(int kind, float *__restrict__ x, int ldx, int rows,
@@ -206,6 +258,39 @@ int launch_splice(hipStream_t s, int rows, int dim, const float *in, int ld_in, 
   SpliceIdx idx = {};
   for (int i = 0; i < n_idx; ++i) idx.v[i] = h_idx[i];
   hipLaunchKernelGGL(splice_kernel, dim3(rows), dim3(256), 0, s, rows, dim, in, ld_in, idx, n_idx, out);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
+int launch_lat_finalize(hipStream_t s, const X6Gemm &a, const float *part, int first, int rows, bool log_softmax,
+                        const float *log_prior, const int *row_dst, float *out) {
+  if (rows <= 0) return CE_GPU_OK;
+  if (!part || !out || a.n % 4 != 0 || a.n > 4 * 64 * kMaxVecPerLane || first < 0 || first + rows > a.m ||
+      a.npost > 4 ||
+      ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(log_prior) |
+        reinterpret_cast<uintptr_t>(a.bias) | reinterpret_cast<uintptr_t>(a.bn_scale) |
+        reinterpret_cast<uintptr_t>(a.bn_offset)) & 15))
+    return fail(CE_GPU_EINVAL, "lat_finalize: bad geometry");
+  LatFinalizeArgs p;
+  p.part = part;
+  p.slices = x6_lat_slices(a.kpad, a.n);
+  p.m = a.m;
+  p.first = first;
+  p.rows = rows;
+  p.dim = a.n;
+  p.bias = a.bias;
+  p.bn_scale = a.bn_scale;
+  p.bn_offset = a.bn_offset;
+  for (int i = 0; i < 4; ++i) p.post[i] = a.post[i];
+  p.npost = a.npost;
+  p.prior = log_prior;
+  p.row_dst = row_dst;
+  p.out = out;
+  const dim3 grid(rows), block(256);
+  if (log_softmax)
+    hipLaunchKernelGGL(lat_finalize_kernel<true>, grid, block, 0, s, p);
+  else
+    hipLaunchKernelGGL(lat_finalize_kernel<false>, grid, block, 0, s, p);
   CE_HIP(hipGetLastError());
   return CE_GPU_OK;
 }

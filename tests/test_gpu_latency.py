@@ -1,10 +1,11 @@
-"""Latency mode (ce_gpu_ctx_set_latency): the fp32 nnet GEMMs split K over
-up to 8 blocks per output tile so a small row block -- the streaming
-AcousticModel::Process chunk (src/am.cc:115-142) or one utterance -- spreads
-over the chip.  Same bars as the default mode: log-likelihoods within 1e-4
-of the oracle, bit-identical across row segmentations and batchings (the
-slice count depends on K only and slices are summed in slice order), and
-deterministic run to run (the last-arriver fix-up never races)."""
+"""Latency mode (ce_gpu_ctx_set_latency, kernels/gemm_bf16x6_lat.hip): the
+fp32 nnet GEMMs split K into slices (x6_lat_slices: a function of K and N
+only, about 256 blocks per 128-row tile block) so a small row block -- the
+streaming AcousticModel::Process chunk (src/am.cc:115-142) or one utterance
+-- spreads over the chip; a reduce kernel sums the slices' partials in slice
+order.  Same bars as the default mode: log-likelihoods within 1e-4 of the
+oracle, bit-identical across row segmentations and batchings, and
+deterministic run to run (no atomics, no inter-block hand-off)."""
 import numpy as np
 import pytest
 

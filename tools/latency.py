@@ -2,7 +2,9 @@
 to back, HIP events), default (throughput) mode vs latency mode
 (ce_gpu_ctx_set_latency): the streaming AcousticModel chunk (chunk_size 50 +
 20 context rows), a 250-frame chunk, one 10 s utterance (1018 rows) and the
-bench's 4072-row batch.   python tools/latency.py [calls]"""
+bench's 4072-row batch.   python tools/latency.py [calls]
+(LAT_MODES=latency LAT_ROWS=70 restrict the modes and row counts)"""
+import hashlib
 import json
 import os
 import sys
@@ -19,11 +21,13 @@ def main(calls=200):
     mdir = os.path.join(tempfile.gettempdir(), f"catears_bench_{os.getuid()}")
     conf = synth.write_model(mdir, "tdnn-s")
     res = {}
-    for mode in ("throughput", "latency"):
+    modes = os.environ.get("LAT_MODES", "throughput,latency").split(",")
+    sizes = [int(v) for v in os.environ.get("LAT_ROWS", "70,270,1018,4072").split(",")]
+    for mode in modes:
         ctx = gpu.Context(0)
         ctx.set_latency(mode == "latency")
         model = gpu.Model(ctx, conf)
-        for rows in (70, 270, 1018, 4072):
+        for rows in sizes:
             x = torch.from_numpy(np.random.default_rng(rows).normal(0, 3, size=(rows, 40)).astype(np.float32)).cuda()
             out = gpu.nnet_propagate(ctx, model, x)
             for _ in range(20):
@@ -37,8 +41,11 @@ def main(calls=200):
             torch.cuda.synchronize()
             us = a.elapsed_time(b) * 1e3 / calls
             frames = rows - model.left - model.right
-            res[f"{mode}/{rows}"] = {"us_per_call": round(us, 1), "frames_per_s": round(frames / us * 1e6)}
-            print(f"{mode:10s} rows {rows:5d}: {us:8.1f} us/call  {frames / us * 1e6 / 1e6:7.3f} M frames/s", flush=True)
+            digest = hashlib.sha1(out.cpu().numpy().tobytes()).hexdigest()[:12]
+            res[f"{mode}/{rows}"] = {"us_per_call": round(us, 1), "frames_per_s": round(frames / us * 1e6),
+                                     "sha1": digest}
+            print(f"{mode:10s} rows {rows:5d}: {us:8.1f} us/call  {frames / us * 1e6 / 1e6:7.3f} M frames/s"
+                  f"  out {digest}", flush=True)
     print(json.dumps(res))
 
 
