@@ -41,16 +41,15 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kLatNW = 4;              // waves per block, 16 units each
 constexpr int kLatBW = 16 * kLatNW;    // units per block
-constexpr int kLatMaxKt = 6;           // K-tiles (of 32) per slice: all its weights in registers
+constexpr int kLatMaxKt = 8;           // K-tiles (of 32) per slice: all its weights in registers
 constexpr int kLatTarget = 256;        // blocks per row tile the slice rule aims at
 
 struct LatArgs {
   const float *xf;
   const uint16_t *wd;
-  const float *wf;
   float *part;
   const int *row_map;
-  int ldx, wd_kt, ldw;
+  int ldx, wd_kt;
   int m, n, kpad, din, nseg;
   uint64_t off_packed;
   int slices, per;  // S, K-tiles per slice
@@ -78,23 +77,18 @@ __device__ __forceinline__ Planes2 split3_pair(float a, float b) {
   return Planes2{p0, p1, cvt(sa, sb)};
 }
 
-// WF: the A fragments from the fp32 weights (n x ldw, K-contiguous: lane l's
-// 8 k of unit 16 u + (l & 15) are 32 contiguous bytes, a wave's load 16 full
-// 128-byte lines) split into planes in registers -- 4 bytes per weight from
-// memory instead of the fragment image's 6; the same planes bit for bit.
-// DIAG (CATEARS_DIAG builds only, tools/ timing breakdowns; wrong results):
-// bit 1 no weight loads, 2 no activation loads, 4 no MFMAs, 8 no stores.
 // MULTI: the block loops over several row tiles (large windows); a single
 // tile is straight-line code (a loop would make the compiler drain the weight
 // loads before the activation loads are issued, at the loop header).
-template <int TF, bool WF, bool MULTI, int DIAG = 0>
-__global__ __launch_bounds__(64 * kLatNW, 1) void lat_gemm_kernel(LatArgs p) {
+// KT: K-tiles per slice the block is sized for (>= the slice's per).
+template <int TF, int KT, bool MULTI, int DIAG = 0>
+__global__ __launch_bounds__(64 * kLatNW, MULTI ? 2 : 1) void lat_gemm_kernel(LatArgs p) {
 #ifndef CATEARS_DIAG
   static_assert(DIAG == 0, "diagnostic schedules are CATEARS_DIAG builds only");
 #endif
   constexpr int BF = 16 * TF;
   constexpr int KSTAGE = 3 * BF * 64;  // bytes: the planes of one K-tile
-  __shared__ __attribute__((aligned(1024))) char smem[kLatMaxKt * KSTAGE];
+  __shared__ __attribute__((aligned(1024))) char smem[KT * KSTAGE];
   typedef const __attribute__((address_space(1))) bf16x8 gfrag;
   typedef const __attribute__((address_space(1))) f32x4 gvec;
   auto swz = [](int row) { return ((row >> 3) & 1) << 1; };
@@ -113,7 +107,7 @@ __global__ __launch_bounds__(64 * kLatNW, 1) void lat_gemm_kernel(LatArgs p) {
   // splits and LDS stores.  A chunk's 8 k lie in one segment (din % 8 == 0);
   // k past the segments is K's zero padding; tasks past the slice load a
   // clamped (valid) address.
-  constexpr int NT = 64 * kLatNW, TASKS = kLatMaxKt * BF * 4, TPT = (TASKS + NT - 1) / NT;
+  constexpr int NT = 64 * kLatNW, TASKS = KT * BF * 4, TPT = (TASKS + NT - 1) / NT;
   gvec *xptr[TPT];
   bool xlive[TPT];
   auto act_addr = [&](int rt) {
@@ -141,24 +135,12 @@ __global__ __launch_bounds__(64 * kLatNW, 1) void lat_gemm_kernel(LatArgs p) {
   __builtin_amdgcn_sched_barrier(0);
 
   // 1. every weight fragment of the slice, at once (units n0 + 16 wave ..)
-  bf16x8 wa[WF ? 1 : kLatMaxKt][3];
-  f32x4 wv[WF ? kLatMaxKt : 1][2];
-  if constexpr (WF) {
-    const int unit = n0 + wave * 16 + (lane & 15);
-    const bool uok = unit < p.n;
-    gvec *wr = (gvec *)(p.wf + (size_t)(uok ? unit : 0) * p.ldw + 8 * (lane >> 4));
-    // branch-free: K-tiles past the slice load the last one (ignored)
-#pragma unroll
-    for (int i = 0; i < kLatMaxKt; ++i) {
-      const int kt = min(kt0 + i, ktiles - 1);
-      wv[i][0] = wr[kt * 8];
-      wv[i][1] = wr[kt * 8 + 1];
-      if (!uok || (DIAG & 1)) wv[i][0] = wv[i][1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    }
-  } else {
+  bf16x8 wa[KT][3];
+  {
     gfrag *wb = (gfrag *)(p.wd + ((size_t)((n0 >> 4) + wave) * p.wd_kt * 3 * 64 + lane) * 8);
+    // branch-free: K-tiles past the slice load the last one (never used)
 #pragma unroll
-    for (int i = 0; i < kLatMaxKt; ++i)
+    for (int i = 0; i < KT; ++i)
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl) {
         wa[i][pl] = wb[(min(kt0 + i, ktiles - 1) * 3 + pl) * 64];
@@ -166,21 +148,6 @@ __global__ __launch_bounds__(64 * kLatNW, 1) void lat_gemm_kernel(LatArgs p) {
       }
   }
   __builtin_amdgcn_sched_barrier(0);
-  // the three planes of K-tile i's A fragment
-  auto afrag = [&](int i, bf16x8 (&w)[3]) {
-    if constexpr (WF) {
-      const f32x4 a = wv[i][0], b = wv[i][1];
-      const Planes2 q0 = split3_pair(a.x, a.y), q1 = split3_pair(a.z, a.w);
-      const Planes2 q2 = split3_pair(b.x, b.y), q3 = split3_pair(b.z, b.w);
-      w[0] = __builtin_bit_cast(bf16x8, u32x4{q0.h, q1.h, q2.h, q3.h});
-      w[1] = __builtin_bit_cast(bf16x8, u32x4{q0.m, q1.m, q2.m, q3.m});
-      w[2] = __builtin_bit_cast(bf16x8, u32x4{q0.l, q1.l, q2.l, q3.l});
-    } else {
-      w[0] = wa[i][0];
-      w[1] = wa[i][1];
-      w[2] = wa[i][2];
-    }
-  };
 
   // the block's row tiles, one after another with the weights kept in
   // registers (a window of many row tiles reads each weight once per block)
@@ -226,11 +193,10 @@ __global__ __launch_bounds__(64 * kLatNW, 1) void lat_gemm_kernel(LatArgs p) {
 #pragma unroll
   for (int j = 0; j < TF; ++j) acc[j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-  for (int i = 0; i < kLatMaxKt; ++i) {
+  for (int i = 0; i < KT; ++i) {
     if (i >= nk) break;
     const char *st = smem + i * KSTAGE;
-    bf16x8 w[3];
-    afrag(i, w);
+    const bf16x8 (&w)[3] = wa[i];
     bf16x8 b0[TF], b1[TF];
 #pragma unroll
     for (int j = 0; j < TF; ++j) b0[j] = *reinterpret_cast<const bf16x8 *>(st + (j * 16) * 64 + foff);
@@ -303,34 +269,21 @@ __global__ __launch_bounds__(64) void lat_reduce_kernel(LatReduceArgs p) {
   *reinterpret_cast<f32x4 *>(p.y + (int64_t)(p.row0 + r) * p.ldy + n) = v;
 }
 
-// Row tiles per block: enough row groups that a window still spreads over the
-// chip, few enough that the weights are not re-read per 80 rows.  The
-// partition changes which block computes a tile, never the tile's sums.
-int lat_rtb(int row_tiles) {
+// Row tiles per block: enough blocks for two per CU (the many-tile kernel's
+// occupancy), the rest looped with the weights kept in registers rather than
+// re-read per tile.  The partition changes which block computes a tile, never
+// the tile's sums.
+int lat_rtb(int row_tiles, int blocks_per_tile) {
   static const int env = [] {
     const char *e = getenv("CATEARS_LAT_RTB");
     return e ? atoi(e) : 0;
   }();
-  const int rtb = env > 0 ? env : 4;
+  const int rtb = env > 0 ? env : row_tiles * blocks_per_tile / (2 * kLatTarget);
   return std::max(1, std::min(rtb, row_tiles));
 }
 
-// The weight source: fp32 weights split in registers (default) or the
-// fragment image (CATEARS_LAT_WSRC=frag) -- the same planes, the same bits.
-bool lat_wf() {
-  static const bool v = [] {
-    const char *e = getenv("CATEARS_LAT_WSRC");
-    return !(e && std::string(e) == "frag");
-  }();
-  return v;
-}
-
-template <int TF>
-void launch_lat_gemm(hipStream_t s, LatArgs p) {
-  p.row_tiles = (p.rows + 16 * TF - 1) / (16 * TF);
-  p.rtb = lat_rtb(p.row_tiles);
-  const int groups = (p.row_tiles + p.rtb - 1) / p.rtb;
-  const dim3 grid(groups * p.tiles_n * p.slices), block(64 * kLatNW);
+template <int TF, int KT>
+void launch_lat_gemm_kt(hipStream_t s, const LatArgs &p, dim3 grid, dim3 block) {
 #ifdef CATEARS_DIAG
   static const int diag = [] {
     const char *e = getenv("CATEARS_LAT_DIAG");
@@ -339,28 +292,41 @@ void launch_lat_gemm(hipStream_t s, LatArgs p) {
   switch (diag) {
     case 0: break;
 #define CE_LAT_DIAG(D) \
-  case D: hipLaunchKernelGGL((lat_gemm_kernel<TF, false, true, D>), grid, block, 0, s, p); return;
+  case D: hipLaunchKernelGGL((lat_gemm_kernel<TF, KT, true, D>), grid, block, 0, s, p); return;
     CE_LAT_DIAG(1) CE_LAT_DIAG(2) CE_LAT_DIAG(3) CE_LAT_DIAG(4) CE_LAT_DIAG(8) CE_LAT_DIAG(12) CE_LAT_DIAG(15)
 #undef CE_LAT_DIAG
     default: break;
   }
 #endif
-  const bool multi = p.rtb > 1;
-  if (p.wf && multi)
-    hipLaunchKernelGGL((lat_gemm_kernel<TF, true, true>), grid, block, 0, s, p);
-  else if (p.wf)
-    hipLaunchKernelGGL((lat_gemm_kernel<TF, true, false>), grid, block, 0, s, p);
-  else if (multi)
-    hipLaunchKernelGGL((lat_gemm_kernel<TF, false, true>), grid, block, 0, s, p);
+  if (p.rtb > 1)
+    hipLaunchKernelGGL((lat_gemm_kernel<TF, KT, true>), grid, block, 0, s, p);
   else
-    hipLaunchKernelGGL((lat_gemm_kernel<TF, false, false>), grid, block, 0, s, p);
+    hipLaunchKernelGGL((lat_gemm_kernel<TF, KT, false>), grid, block, 0, s, p);
+}
+
+template <int TF>
+void launch_lat_gemm(hipStream_t s, LatArgs p) {
+  p.row_tiles = (p.rows + 16 * TF - 1) / (16 * TF);
+  p.rtb = lat_rtb(p.row_tiles, p.tiles_n * p.slices);
+  const int groups = (p.row_tiles + p.rtb - 1) / p.rtb;
+  const dim3 grid(groups * p.tiles_n * p.slices), block(64 * kLatNW);
+  // the block sized for the slice (its weights all in registers)
+  if (p.per <= 2)
+    launch_lat_gemm_kt<TF, 2>(s, p, grid, block);
+  else if (p.per <= 4)
+    launch_lat_gemm_kt<TF, 4>(s, p, grid, block);
+  else if (p.per <= 6)
+    launch_lat_gemm_kt<TF, 6>(s, p, grid, block);
+  else
+    launch_lat_gemm_kt<TF, 8>(s, p, grid, block);
 }
 
 }  // namespace
 
 int x6_lat_slices(int kpad, int n) {
   const int ktiles = kpad / 32, cols = (n + kLatBW - 1) / kLatBW;
-  int slices = std::max(1, std::min(ktiles, (kLatTarget + cols / 2) / cols));
+  // at most kLatTarget blocks per row tile (one wave of blocks over the CUs)
+  int slices = std::max(1, std::min(ktiles, kLatTarget / cols));
   int per = (ktiles + slices - 1) / slices;
   per = std::min(per, kLatMaxKt);
   return (ktiles + per - 1) / per;  // no empty slice
@@ -383,8 +349,6 @@ int launch_gemm_bf16x6_lat(hipStream_t s, const X6Gemm &a, float *part, size_t p
   LatArgs p;
   p.xf = a.xf;
   p.wd = a.wd;
-  p.wf = lat_wf() && a.wf && a.ldw % 4 == 0 && (reinterpret_cast<uintptr_t>(a.wf) & 15) == 0 ? a.wf : nullptr;
-  p.ldw = a.ldw;
   p.part = part;
   p.ldx = a.ldx;
   p.wd_kt = a.wd_kt;
@@ -422,8 +386,10 @@ int launch_gemm_bf16x6_lat(hipStream_t s, const X6Gemm &a, float *part, size_t p
     // the frame tile fitting the block (results do not depend on it)
     if (p.rows <= 32)
       launch_lat_gemm<2>(s, p);
-    else
+    else if (p.rows <= 80)
       launch_lat_gemm<5>(s, p);
+    else
+      launch_lat_gemm<4>(s, p);  // many row tiles: 64-row tiles, two blocks per CU
     CE_HIP(hipGetLastError());
     if (!reduce) break;
     const int64_t threads = (int64_t)p.rows * (a.n / 4);

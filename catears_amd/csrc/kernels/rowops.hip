@@ -10,6 +10,8 @@
 //   reference's converter, but legal NN02).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "../internal.h"
 
 namespace catears {
@@ -77,8 +79,14 @@ __device__ __forceinline__ void finalize_row_vec(Load &&load, int dim, const flo
   float4 *o = reinterpret_cast<float4 *>(o_row);
   const float4 *pr = reinterpret_cast<const float4 *>(prior);
   const int d4 = dim >> 2;
-  float4 v[kMaxVecPerLane];
+  float4 v[kMaxVecPerLane], pv[kMaxVecPerLane];
   float s = 0.0f;
+  // the prior's chunks loaded up front with the row (branch-free, clamped),
+  // so the stores below wait on nothing
+  if (prior) {
+#pragma unroll
+    for (int j = 0; j < kMaxVecPerLane; ++j) pv[j] = pr[min(lane + 64 * j, d4 - 1)];
+  }
 #pragma unroll
   for (int j = 0; j < kMaxVecPerLane; ++j) {
     const int c = lane + 64 * j;
@@ -93,7 +101,7 @@ __device__ __forceinline__ void finalize_row_vec(Load &&load, int dim, const flo
       float4 y = v[j];
       if (LOGSM) y = make_float4(y.x - ls, y.y - ls, y.z - ls, y.w - ls);
       if (prior) {
-        const float4 p = pr[c];
+        const float4 p = pv[j];
         y = make_float4(y.x - p.x, y.y - p.y, y.z - p.z, y.w - p.w);
       }
       o[c] = y;
@@ -131,7 +139,7 @@ struct LatFinalizeArgs {
 // One block per row: the 256 threads reduce the row's float4 chunks into LDS
 // (the slice loads of the whole row in flight together), then wave 0 runs the
 // finalize row math on them.
-template <bool LOGSM>
+template <bool LOGSM, int MODE>
 __global__ __launch_bounds__(256) void lat_finalize_kernel(LatFinalizeArgs p) {
   __shared__ float4 vals[64 * kMaxVecPerLane];
   const int row = blockIdx.x, tid = threadIdx.x;
@@ -139,21 +147,49 @@ __global__ __launch_bounds__(256) void lat_finalize_kernel(LatFinalizeArgs p) {
   if (dst < 0) return;  // block-uniform
   const float *src = p.part + (size_t)(p.first + row) * p.dim;
   const size_t stride = (size_t)p.m * p.dim;
-  auto reduce = [&](int c) {
-    const float4 s4 = lat_slice_sum(src + 4 * c, stride, p.slices);
-    const float4 b = p.bias ? reinterpret_cast<const float4 *>(p.bias)[c] : make_float4(-0.0f, -0.0f, -0.0f, -0.0f);
-    float4 sc = make_float4(1.0f, 1.0f, 1.0f, 1.0f), of = make_float4(-0.0f, -0.0f, -0.0f, -0.0f);
-    if (p.npost) {
-      if (p.bn_scale) sc = reinterpret_cast<const float4 *>(p.bn_scale)[c];
-      if (p.bn_offset) of = reinterpret_cast<const float4 *>(p.bn_offset)[c];
-    }
-    return make_float4(apply_post<kPostModeGeneric>(s4.x + b.x, sc.x, of.x, p.post, p.npost),
-                       apply_post<kPostModeGeneric>(s4.y + b.y, sc.y, of.y, p.post, p.npost),
-                       apply_post<kPostModeGeneric>(s4.z + b.z, sc.z, of.z, p.post, p.npost),
-                       apply_post<kPostModeGeneric>(s4.w + b.w, sc.w, of.w, p.post, p.npost));
-  };
   const int d4 = p.dim >> 2;
-  for (int c = tid; c < d4; c += 256) vals[c] = reduce(c);
+  // every thread's chunks x four slices in flight per step (branch-free:
+  // clamped indices), summed in slice order -- lat_slice_sum's arithmetic
+  constexpr int CPT = 64 * kMaxVecPerLane / 256;
+  float4 sum[CPT], bv[CPT], scv[CPT], ofv[CPT];
+  // bias / BatchNorm chunks first (branch-free, clamped): in flight with the
+  // partials rather than one round trip per chunk after them
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) {
+    const int c = min(tid + 256 * j, d4 - 1);
+    bv[j] = p.bias ? reinterpret_cast<const float4 *>(p.bias)[c] : make_float4(-0.0f, -0.0f, -0.0f, -0.0f);
+    scv[j] = p.npost && p.bn_scale ? reinterpret_cast<const float4 *>(p.bn_scale)[c] : make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+    ofv[j] = p.npost && p.bn_offset ? reinterpret_cast<const float4 *>(p.bn_offset)[c]
+                                    : make_float4(-0.0f, -0.0f, -0.0f, -0.0f);
+  }
+  for (int s0 = 0; s0 < p.slices; s0 += 4) {
+    float4 v[CPT][4];
+#pragma unroll
+    for (int j = 0; j < CPT; ++j)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int c = min(tid + 256 * j, d4 - 1), ss = min(s0 + u, p.slices - 1);
+        v[j][u] = *reinterpret_cast<const float4 *>(src + (size_t)ss * stride + 4 * c);
+      }
+#pragma unroll
+    for (int j = 0; j < CPT; ++j)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (s0 + u < p.slices)
+          sum[j] = s0 + u == 0 ? v[j][u]
+                               : make_float4(sum[j].x + v[j][u].x, sum[j].y + v[j][u].y, sum[j].z + v[j][u].z,
+                                             sum[j].w + v[j][u].w);
+  }
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) {
+    const int c = tid + 256 * j;
+    if (c >= d4) break;
+    const float4 s4 = sum[j], b = bv[j], sc = scv[j], of = ofv[j];
+    vals[c] = make_float4(apply_post<MODE>(s4.x + b.x, sc.x, of.x, p.post, p.npost),
+                          apply_post<MODE>(s4.y + b.y, sc.y, of.y, p.post, p.npost),
+                          apply_post<MODE>(s4.z + b.z, sc.z, of.z, p.post, p.npost),
+                          apply_post<MODE>(s4.w + b.w, sc.w, of.w, p.post, p.npost));
+  }
   __syncthreads();
   if (tid >= 64) return;
   finalize_row_vec<LOGSM>([&](int c) { return vals[c]; }, p.dim, p.prior, p.out + (int64_t)dst * p.dim, tid);
@@ -287,10 +323,25 @@ int launch_lat_finalize(hipStream_t s, const X6Gemm &a, const float *part, int f
   p.row_dst = row_dst;
   p.out = out;
   const dim3 grid(rows), block(256);
+  auto go = [&](auto ls) {
+    constexpr bool LS = decltype(ls)::value;
+    switch (post_mode(a.post, a.npost)) {
+      case kPostModeNone: hipLaunchKernelGGL((lat_finalize_kernel<LS, kPostModeNone>), grid, block, 0, s, p); break;
+      case kPostModeRelu: hipLaunchKernelGGL((lat_finalize_kernel<LS, kPostModeRelu>), grid, block, 0, s, p); break;
+      case kPostModeBn: hipLaunchKernelGGL((lat_finalize_kernel<LS, kPostModeBn>), grid, block, 0, s, p); break;
+      case kPostModeReluBn:
+        hipLaunchKernelGGL((lat_finalize_kernel<LS, kPostModeReluBn>), grid, block, 0, s, p);
+        break;
+      case kPostModeBnRelu:
+        hipLaunchKernelGGL((lat_finalize_kernel<LS, kPostModeBnRelu>), grid, block, 0, s, p);
+        break;
+      default: hipLaunchKernelGGL((lat_finalize_kernel<LS, kPostModeGeneric>), grid, block, 0, s, p); break;
+    }
+  };
   if (log_softmax)
-    hipLaunchKernelGGL(lat_finalize_kernel<true>, grid, block, 0, s, p);
+    go(std::true_type());
   else
-    hipLaunchKernelGGL(lat_finalize_kernel<false>, grid, block, 0, s, p);
+    go(std::false_type());
   CE_HIP(hipGetLastError());
   return CE_GPU_OK;
 }

@@ -3,7 +3,7 @@
 # 1 no weight loads, 2 no activation loads, 4 no MFMAs, 8 no stores.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}" && mkdir -p gpurun_out/latdiag && export TMPDIR=/tmp
-for d in 0 1 2 3 4 8 12 15; do
+for d in 0 1 2 3 4; do
   rm -rf gpurun_out/latdiag/run
   CATEARS_HIP_LIB=catears_amd/lib/libcatears_hip_exp.so CATEARS_LAT_DIAG=$d LAT_MODES=latency LAT_ROWS=70 \
     timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/latdiag/run -o run -- \
