@@ -1095,6 +1095,9 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
       case 200:  // warp-specialised: 4 MFMA waves (64 x 64 each) + 4 producer waves
         return launch_ws<X6Cfg<128, 128, 2, 2, 2>, 4>(s, p);
 #ifdef CATEARS_EXPERIMENTS
+      case 302:  // direct weights, 128 x 128 tiles (twice the blocks of 300)
+        if (!a.wd) return fail(CE_GPU_EINVAL, "variant 302 needs the weight fragment image");
+        return launch_d<X6Cfg<128, 128, 2, 4, 2>>(s, p);
       case 42:  // round-1 default: split of tile kt+1, then the MFMAs of tile kt
         return launch_f<X6Cfg<128, 256, 2, 4, 2>>(s, p);
       case 55:  // MFMAs of tile kt first, the split interleaved by the compiler
