@@ -82,7 +82,7 @@ __device__ __forceinline__ Planes2 split3_pair(float a, float b) {
 // loads before the activation loads are issued, at the loop header).
 // KT: K-tiles per slice the block is sized for (>= the slice's per).
 template <int TF, int KT, bool MULTI, int DIAG = 0>
-__global__ __launch_bounds__(64 * kLatNW, MULTI ? 2 : 1) void lat_gemm_kernel(LatArgs p) {
+__global__ __launch_bounds__(64 * kLatNW, MULTI && TF == 4 && KT <= 6 ? 2 : 1) void lat_gemm_kernel(LatArgs p) {
 #ifndef CATEARS_DIAG
   static_assert(DIAG == 0, "diagnostic schedules are CATEARS_DIAG builds only");
 #endif

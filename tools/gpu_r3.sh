@@ -57,15 +57,37 @@ for st in ${STAGE:-tests bench c4}; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c2 -o run -- \
           python3 bench.py --workload c2 --fbank fast --steps 20 --warmup 3 --no-cpu-baseline > $OUT/bench_c2.log 2>&1 || { tail -5 $OUT/bench_c2.log; exit 1; }
       grep '^{' $OUT/bench_c2.log | cut -c1-200
+      # both fbank modes' kernels in one summary (runs under one parent dir)
       i=0
       for grp in FETCH_SIZE WRITE_SIZE; do
         i=$((i+1))
-        timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-include-regex "fbank" --output-format csv -d $OUT/pmc_c2_$i -o run -- \
-            python3 bench.py --workload c2 --fbank fast --steps 3 --warmup 1 --no-cpu-baseline --no-profile > $OUT/pmc_c2_$i.log 2>&1 \
-            || { echo "pmc c2 $i failed"; tail -5 $OUT/pmc_c2_$i.log; exit 1; }
+        for m in exact fast; do
+          timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-include-regex "fbank" --output-format csv -d $OUT/pmc_c2_$i/$m -o run -- \
+              python3 bench.py --workload c2 --fbank $m --steps 3 --warmup 1 --no-cpu-baseline --no-profile > $OUT/pmc_c2_$i.$m.log 2>&1 \
+              || { echo "pmc c2 $i $m failed"; tail -5 $OUT/pmc_c2_$i.$m.log; exit 1; }
+        done
       done
       python3 tools/pmc_traffic.py $OUT/pmc_c2_1 $OUT/pmc_c2_2 $OUT/pmc_traffic_c2.json
-      cat $OUT/pmc_traffic_c2.json | head -20 ;;
+      cat $OUT/pmc_traffic_c2.json | head -20
+      # C5 (int8): kernel trace + stats of the pipelined line, PMC traffic and
+      # MFMA busy of its GEMMs on a serial run
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_c5 -o run -- \
+          python3 bench.py --workload c5 --steps 60 --warmup 10 --no-cpu-baseline > $OUT/bench_c5.log 2>&1 || { tail -5 $OUT/bench_c5.log; exit 1; }
+      grep '^{' $OUT/bench_c5.log | cut -c1-200
+      i=0
+      for grp in FETCH_SIZE WRITE_SIZE; do
+        i=$((i+1))
+        timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-include-regex "gemm_|quantize|minmax|finalize" --output-format csv -d $OUT/pmc_c5_$i -o run -- \
+            python3 bench.py --workload c5 --steps 4 --warmup 1 --no-cpu-baseline --no-profile --serial > $OUT/pmc_c5_$i.log 2>&1 \
+            || { echo "pmc c5 $i failed"; tail -5 $OUT/pmc_c5_$i.log; exit 1; }
+      done
+      python3 tools/pmc_traffic.py $OUT/pmc_c5_1 $OUT/pmc_c5_2 $OUT/pmc_traffic_c5.json
+      timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "gemm_" \
+          --output-format csv -d $OUT/pmc_c5_3 -o run -- \
+          python3 bench.py --workload c5 --steps 4 --warmup 1 --no-cpu-baseline --no-profile --serial > $OUT/pmc_c5_3.log 2>&1 \
+          || { echo "pmc c5 3 failed"; tail -5 $OUT/pmc_c5_3.log; exit 1; }
+      python3 tools/pmc_mfma.py $OUT/pmc_c5_3 $OUT/pmc_mfma_c5.json
+      head -20 $OUT/pmc_mfma_c5.json ;;
     lat)
       CALLS=${CALLS:-100} bash tools/trace_latency.sh || exit 1
       python3 tools/trace_summary.py gpurun_out/lat/kernel_trace.csv "latency.py trace" > gpurun_out/lat/kernel_summary.txt
