@@ -337,17 +337,19 @@ __global__ __launch_bounds__(256, 2) void gemm_i8_nnet_kernel(I8Args p) {
 // A 32x32x32 i8 MFMA operand is one ds_read_b128 per lane (row r, bytes
 // 16h..16h+15 of its 32-byte k-step), so a tile row of 128 bytes holds the
 // four k-steps of the tile.  BM x BN block tile, 2 x 2 waves.
-template <int BM, int BN, int STAGES, int WGM = 2, int WGN = 2>
+template <int BM, int BN, int STAGES, int WGM = 2, int WGN = 2, int BKB = 128>
 __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_i8_glds_kernel(I8Args p) {
   constexpr int NW = WGM * WGN;
-  constexpr int BKB = 128;                  // bytes per K-tile row
+  // BKB: bytes per K-tile row (128, or 64 so a 256 x 256 tile fits 4 stages)
+  constexpr int CH = BKB / 16;              // 16-byte chunks per row
   constexpr int TI = BM / WGM / 32, TJ = BN / WGN / 32;
-  constexpr int RPI = 1024 / BKB;           // rows per DMA instruction (8)
+  constexpr int RPI = 1024 / BKB;           // rows per DMA instruction
   constexpr int NGA = BM * BKB / 1024 / NW, NGB = BN * BKB / 1024 / NW;
   constexpr int STAGE = (BM + BN) * BKB;    // bytes
   static_assert(NGA >= 1 && NGB >= 1 && TI >= 1 && TJ >= 1, "tile too small");
+  static_assert(BKB == 128 || BKB == 64, "K-tile of 64 or 128 bytes");
   __shared__ __attribute__((aligned(1024))) int8_t smem[STAGES * STAGE];
-  auto swz = [](int row) { return (row >> 1) & 7; };
+  auto swz = [](int row) { return (row >> 1) & (CH - 1); };
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN, r = lane & 31, h = lane >> 5;
@@ -355,7 +357,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_i8_glds_kernel(I8Args 
   tile_of(blockIdx.x, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
   const int m0 = tm * BM, n0 = tn * BN;
 
-  const int lrow = lane / 8, lchunk = lane & 7;
+  const int lrow = lane / CH, lchunk = lane & (CH - 1);
   uint32_t boff[NGB];
 #pragma unroll
   for (int j = 0; j < NGB; ++j) {
@@ -740,6 +742,17 @@ int launch_i8_gemm(hipStream_t s, const I8Layer &L, const int8_t *a, int lda, in
       // DMA round trip per iteration, not by MFMA issue
       case 8: go(gemm_i8_glds_kernel<128, 256, 2, 2, 4>, 128, 256, 512); break;
       case 9: go(gemm_i8_glds_kernel<256, 256, 2, 4, 2>, 256, 256, 512); break;
+      // 40-42: 256 x 256 tiles on 64-byte K-tiles (half the L2 bytes per
+      // MFMA of 15), 3 / 4 stages; 16 waves of 64 x 64 (42)
+      case 40: go(gemm_i8_glds_kernel<256, 256, 4, 4, 2, 64>, 256, 256, 512); break;
+      case 41: go(gemm_i8_glds_kernel<256, 256, 3, 4, 2, 64>, 256, 256, 512); break;
+      case 43: go(gemm_i8_glds_kernel<128, 256, 4, 2, 4, 64>, 128, 256, 512); break;
+      case 44: go(gemm_i8_glds_kernel<256, 128, 4, 4, 2, 64>, 256, 128, 512); break;
+      // 45-47: 256 x 256 tiles, 4 waves of 128 x 128 (accumulators in AGPRs):
+      // one fragment read per two MFMAs instead of one per MFMA
+      case 45: go(gemm_i8_glds_kernel<256, 256, 2, 2, 2, 128>, 256, 256, 256); break;
+      case 46: go(gemm_i8_glds_kernel<256, 256, 4, 2, 2, 64>, 256, 256, 256); break;
+      case 47: go(gemm_i8_glds_kernel<256, 256, 3, 2, 2, 64>, 256, 256, 256); break;
       case 10: go(gemm_i8_reg_kernel<128, 128, 2, 2>, 128, 128, 256); break;
       case 11: go(gemm_i8_reg_kernel<256, 128, 4, 2>, 256, 128, 512); break;
       // 20-22: branch-free, DMA two K-tiles ahead (gemm_i8_q_kernel)
