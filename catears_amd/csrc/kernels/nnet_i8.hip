@@ -213,6 +213,7 @@ struct I8Args {
   float *y;
   int ldy;
   int tiles_n, tiles_m, group;
+  int vec_epi;              // i8_epilogue_v (16-byte row stores)
 };
 
 // Zero-point restore + bias + ReLU / BatchNorm + store of one wave's
@@ -267,6 +268,82 @@ __device__ __forceinline__ void i8_epilogue(const I8Args &p, const i32x16 (&acc)
           if (m0 + lr < p.m) p.y[(int64_t)(m0 + lr) * p.ldy + col] = y;
         }
       }
+    }
+  });
+}
+
+// The same epilogue with the stores vectorised: each wave finishes its tile
+// one 32-row slab at a time into a wave-private LDS slab (row stride padded
+// by 32 B so the two row groups of a write land in different banks), then
+// writes the slab back as 16-byte row chunks -- a quarter of the store
+// instructions of i8_epilogue, whose 4-byte column stores made the epilogue
+// store-issue bound.  Same values, same bits.  Needs n % 4 ==
+// 0 and ldy % 4 == 0 (host-checked) and NW slabs of 32 x (TJ 32 + 8) floats
+// plus BM words of row sums in `lds`.
+template <int TI, int TJ, int BM, int NT>
+__device__ __forceinline__ void i8_epilogue_v(const I8Args &p, const i32x16 (&acc)[TI][TJ], int m0, int wrow,
+                                              int col0, int r, int h, char *lds) {
+  constexpr int NW = NT / 64, SW = TJ * 32 + 8;  // slab row stride, floats
+  const QP pa = *static_cast<const QP *>(p.pa);
+  const uint32_t ca = (uint32_t)(128 - pa.zp), cb = (uint32_t)(128 - p.w_zp);
+  const uint32_t kterm = (uint32_t)p.k * ca * cb;
+  const float cscale = pa.scale * p.w_scale;  // matrix.cc:404-405
+  uint32_t *srs = reinterpret_cast<uint32_t *>(lds + NW * 32 * SW * 4);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float *slab = reinterpret_cast<float *>(lds) + wave * 32 * SW;
+  __syncthreads();
+  for (int t = threadIdx.x; t < BM; t += NT) {
+    const int row = m0 + t;
+    uint32_t sum = 0;
+#pragma unroll
+    for (int sg = 0; sg < 8; ++sg) {
+      if (sg < p.nseg) {
+        int src = row + p.off[sg];
+        src = src < 0 ? 0 : (src > p.m - 1 ? p.m - 1 : src);
+        sum += (uint32_t)p.rowsum[src];
+      }
+    }
+    srs[t] = cb * sum;
+  }
+  __syncthreads();
+  // column constants of this lane's TJ columns, loaded once
+  uint32_t cterm[TJ];
+  float bias[TJ], sc[TJ], of[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int col = min(col0 + j * 32 + r, p.n - 1);
+    cterm[j] = ca * (uint32_t)p.colsum[col] + kterm;
+    bias[j] = p.bias ? p.bias[col] : 0.0f;
+    sc[j] = p.bn_scale ? p.bn_scale[col] : 1.0f;
+    of[j] = p.bn_offset ? p.bn_offset[col] : 0.0f;
+  }
+  constexpr int C4 = TJ * 8;  // float4 chunks per slab row
+  with_post_mode(p.post_mode, [&](auto M) {
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int rr = (e & 3) + 8 * (e >> 2) + 4 * h;  // row within the slab
+          const uint32_t v = (uint32_t)acc[i][j][e] + srs[wrow + i * 32 + rr] + cterm[j];
+          float y = (float)(int32_t)v * cscale;
+          y = y + bias[j];  // +0 when absent: y is never -0 here (int * positive scale)
+          slab[rr * SW + j * 32 + r] = apply_post<decltype(M)::value>(y, sc[j], of[j], p.post, p.npost);
+        }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int q = 0; q < 32 * C4 / 64; ++q) {
+        const int idx = lane + 64 * q, rr = idx / C4, c4 = idx % C4;
+        const int row = m0 + wrow + i * 32 + rr, col = col0 + 4 * c4;
+        const float4 v = *reinterpret_cast<const float4 *>(slab + rr * SW + 4 * c4);
+        if (row < p.m && col < p.n) *reinterpret_cast<float4 *>(p.y + (int64_t)row * p.ldy + col) = v;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   });
 }
@@ -337,8 +414,14 @@ __global__ __launch_bounds__(256, 2) void gemm_i8_nnet_kernel(I8Args p) {
 // A 32x32x32 i8 MFMA operand is one ds_read_b128 per lane (row r, bytes
 // 16h..16h+15 of its 32-byte k-step), so a tile row of 128 bytes holds the
 // four k-steps of the tile.  BM x BN block tile, 2 x 2 waves.
-template <int BM, int BN, int STAGES, int WGM = 2, int WGN = 2, int BKB = 128>
+// DIAG (CATEARS_DIAG builds only: timing breakdowns, wrong results): bit 1
+// no DMA after the prologue, 2 no MFMAs (fragment reads kept live), 4 no
+// fragment reads (MFMAs on constant operands).
+template <int BM, int BN, int STAGES, int WGM = 2, int WGN = 2, int BKB = 128, int DIAG = 0>
 __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_i8_glds_kernel(I8Args p) {
+#ifndef CATEARS_DIAG
+  static_assert(DIAG == 0, "diagnostic schedules are CATEARS_DIAG builds only");
+#endif
   constexpr int NW = WGM * WGN;
   // BKB: bytes per K-tile row (128, or 64 so a 256 x 256 tile fits 4 stages)
   constexpr int CH = BKB / 16;              // 16-byte chunks per row
@@ -420,16 +503,25 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_i8_glds_kernel(I8Args 
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (kt + STAGES - 1 < ktiles) issue(kt + STAGES - 1);
+    if (!(DIAG & 1) && kt + STAGES - 1 < ktiles) issue(kt + STAGES - 1);
     const int8_t *st = smem + (kt % STAGES) * STAGE;
 #pragma unroll
     for (int s = 0; s < BKB / 32; ++s) {
       const int ch = ((2 * s) ^ xr) * 16;
       i32x4 af[TI], bf[TJ];
 #pragma unroll
-      for (int i = 0; i < TI; ++i) af[i] = *reinterpret_cast<const i32x4 *>(st + a_row + i * 32 * BKB + ch);
+      for (int i = 0; i < TI; ++i)
+        af[i] = (DIAG & 4) ? i32x4{kt, s, i, 1} : *reinterpret_cast<const i32x4 *>(st + a_row + i * 32 * BKB + ch);
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) bf[j] = *reinterpret_cast<const i32x4 *>(st + b_row + j * 32 * BKB + ch);
+      for (int j = 0; j < TJ; ++j)
+        bf[j] = (DIAG & 4) ? i32x4{s, kt, j, 2} : *reinterpret_cast<const i32x4 *>(st + b_row + j * 32 * BKB + ch);
+      if constexpr ((DIAG & 2) != 0) {
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) acc[i][j][0] ^= af[i][0] ^ bf[j][1];
+        continue;
+      }
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -438,7 +530,24 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_i8_glds_kernel(I8Args 
     }
   }
 
-  i8_epilogue<TI, TJ, BM, 64 * NW>(p, acc, m0, wm * TI * 32, n0 + wn * TJ * 32, r, h, reinterpret_cast<uint32_t *>(smem));
+  if constexpr ((DIAG & 8) != 0) {  // no epilogue: one word per lane keeps the loop live
+    int t = 0;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) t ^= acc[i][j][e];
+    p.y[(int64_t)blockIdx.x * 64 * NW + tid] = (float)t;
+    return;
+  }
+  constexpr bool kVecFits = NW * 32 * (TJ * 32 + 8) * 4 + BM * 4 <= STAGES * STAGE;  // slabs in the stages
+  if (kVecFits && p.vec_epi)
+    i8_epilogue_v<TI, TJ, BM, 64 * NW>(p, acc, m0, wm * TI * 32, n0 + wn * TJ * 32, r, h,
+                                       reinterpret_cast<char *>(smem));
+  else
+    i8_epilogue<TI, TJ, BM, 64 * NW>(p, acc, m0, wm * TI * 32, n0 + wn * TJ * 32, r, h,
+                                     reinterpret_cast<uint32_t *>(smem));
 }
 
 
@@ -712,6 +821,11 @@ int launch_i8_gemm(hipStream_t s, const I8Layer &L, const int8_t *a, int lda, in
   p.post_mode = post_mode(L.post, L.npost);
   p.y = y;
   p.ldy = ldy;
+  static const int vec_epi = [] {
+    const char *e = getenv("CATEARS_I8_EPI");
+    return e ? atoi(e) : 1;
+  }();
+  p.vec_epi = vec_epi && L.n % 4 == 0 && ldy % 4 == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0;
   static const int use_glds = [] {
     const char *e = getenv("CATEARS_I8_GEMM");
     return e ? atoi(e) : 15;  // measured best on TDNN-S, frame batch 8192 (tools/i8_sweep.sh)
@@ -751,8 +865,21 @@ int launch_i8_gemm(hipStream_t s, const I8Layer &L, const int8_t *a, int lda, in
       // 45-47: 256 x 256 tiles, 4 waves of 128 x 128 (accumulators in AGPRs):
       // one fragment read per two MFMAs instead of one per MFMA
       case 45: go(gemm_i8_glds_kernel<256, 256, 2, 2, 2, 128>, 256, 256, 256); break;
+#ifdef CATEARS_DIAG
+      // timing-only ablations of 15 (wrong results)
+      case 61: go(gemm_i8_glds_kernel<256, 128, 3, 4, 2, 128, 1>, 256, 128, 512); break;
+      case 62: go(gemm_i8_glds_kernel<256, 128, 3, 4, 2, 128, 2>, 256, 128, 512); break;
+      case 64: go(gemm_i8_glds_kernel<256, 128, 3, 4, 2, 128, 4>, 256, 128, 512); break;
+      case 65: go(gemm_i8_glds_kernel<256, 128, 3, 4, 2, 128, 5>, 256, 128, 512); break;
+      case 63: go(gemm_i8_glds_kernel<256, 128, 3, 4, 2, 128, 3>, 256, 128, 512); break;
+      case 68: go(gemm_i8_glds_kernel<256, 128, 3, 4, 2, 128, 8>, 256, 128, 512); break;
+      case 71: go(gemm_i8_glds_kernel<256, 128, 3, 4, 2, 128, 11>, 256, 128, 512); break;
+#endif
       case 46: go(gemm_i8_glds_kernel<256, 256, 4, 2, 2, 64>, 256, 256, 256); break;
       case 47: go(gemm_i8_glds_kernel<256, 256, 3, 2, 2, 64>, 256, 256, 256); break;
+      // 48-49: 256 x 256, 8 waves of 128 x 64 (0.75 fragment reads per MFMA)
+      case 48: go(gemm_i8_glds_kernel<256, 256, 3, 2, 4, 64>, 256, 256, 512); break;
+      case 49: go(gemm_i8_glds_kernel<256, 256, 4, 2, 4, 64>, 256, 256, 512); break;
       case 10: go(gemm_i8_reg_kernel<128, 128, 2, 2>, 128, 128, 256); break;
       case 11: go(gemm_i8_reg_kernel<256, 128, 4, 2>, 256, 128, 512); break;
       // 20-22: branch-free, DMA two K-tiles ahead (gemm_i8_q_kernel)
