@@ -183,7 +183,7 @@ SPLIT_DTYPE = {
              "significant bits, 3 MFMA products in 2 fp32 accumulators; error vs oracle at the fp32-MFMA "
              "path's level, tests/test_gpu_parity.py)",
 }
-I8_ROOFLINE_KERNEL = "gemm_i8_glds_kernel<256, 128, 3, 4, 2>"  # CATEARS_I8_GEMM default (nnet_i8.hip)
+I8_ROOFLINE_KERNEL = "gemm_i8_glds_kernel<256, 128, 3, 4, 2, 128, 0>"  # CATEARS_I8_GEMM default (nnet_i8.hip)
 
 
 def gemm_algorithmic_bytes(rows, layers=((3072, 1024),) * 4 + ((1024, 1024), (1024, 3456))):
