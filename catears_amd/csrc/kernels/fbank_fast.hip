@@ -145,7 +145,11 @@ __global__ __launch_bounds__(kWaves * 64, 3) void fbank_fast_kernel(const FbankT
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int g = lane >> 4, j = lane & 15;
   float2 *R = sm.frame[wave] + g * kRegion;  // this frame's LDS region
-  float *P = reinterpret_cast<float *>(R);   // the power spectrum reuses it
+  // the power spectrum reuses the region, 16 dwords in for odd frames: the
+  // regions are 544 dwords apart (= 0 mod 32), so frames 2i and 2i+1 -- one
+  // 32-lane group of a ds_read_b32 / ds_write_b32 -- would otherwise read and
+  // write every bin on the same bank
+  float *P = reinterpret_cast<float *>(R) + 16 * (g & 1);
   const int64_t stride = (int64_t)gridDim.x * kFramesPerBlk;
   for (int64_t fb = ((int64_t)blockIdx.x * kWaves + wave) * kFramesPerWave; fb < total_frames; fb += stride) {
     const int64_t fr = fb + g;

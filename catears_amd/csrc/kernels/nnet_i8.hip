@@ -880,6 +880,8 @@ int launch_i8_gemm(hipStream_t s, const I8Layer &L, const int8_t *a, int lda, in
       // 48-49: 256 x 256, 8 waves of 128 x 64 (0.75 fragment reads per MFMA)
       case 48: go(gemm_i8_glds_kernel<256, 256, 3, 2, 4, 64>, 256, 256, 512); break;
       case 49: go(gemm_i8_glds_kernel<256, 256, 4, 2, 4, 64>, 256, 256, 512); break;
+      case 50: go(gemm_i8_glds_kernel<256, 256, 2, 2, 4, 128>, 256, 256, 512); break;
+      case 51: go(gemm_i8_glds_kernel<256, 128, 2, 2, 4, 128>, 256, 128, 512); break;
       case 10: go(gemm_i8_reg_kernel<128, 128, 2, 2>, 128, 128, 256); break;
       case 11: go(gemm_i8_reg_kernel<256, 128, 4, 2>, 256, 128, 512); break;
       // 20-22: branch-free, DMA two K-tiles ahead (gemm_i8_q_kernel)

@@ -128,6 +128,7 @@ class Runtime {
   Lane *NewLane();
   int device_ = 0;
   int max_lanes_ = 4;
+  int fbank_mode_ = 0;  // CE_GPU_FBANK_EXACT, or _FAST from CATEARS_FBANK
   mutable std::mutex pool_mu_;
   Lane *lanes_[16] = {nullptr};
   int n_lanes_ = 0;

@@ -7,6 +7,7 @@
 #include <stdlib.h>
 
 #include <atomic>
+#include <string>
 
 namespace catears {
 namespace host {
@@ -87,6 +88,7 @@ Runtime::Lane *Runtime::NewLane() {
   hip_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
   l->stream = s;
   Check(ce_gpu_ctx_create(device_, l->stream, &l->ctx), "ce_gpu_ctx_create");
+  Check(ce_gpu_ctx_set_fbank(l->ctx, fbank_mode_), "ce_gpu_ctx_set_fbank");
   lanes_[n_lanes_++] = l;
   return l;
 }
@@ -98,6 +100,16 @@ Runtime::Runtime() {
     const int v = atoi(e);
     if (v < 1 || v > 16) throw DeviceError("CATEARS_LANES must be 1..16");
     max_lanes_ = v;
+  }
+  // CATEARS_FBANK=fast: every lane's fbank launches take the four-step-FFT
+  // kernel (ce_gpu_ctx_set_fbank); "exact" (the default) keeps the
+  // reference's operation order
+  if (const char *e = getenv("CATEARS_FBANK")) {
+    const std::string v(e);
+    if (v == "fast")
+      fbank_mode_ = CE_GPU_FBANK_FAST;
+    else if (v != "exact")
+      throw DeviceError("CATEARS_FBANK must be \"exact\" or \"fast\"");
   }
   NewLane();  // lane 0: the layer-level paths and model loading
 }

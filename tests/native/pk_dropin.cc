@@ -80,7 +80,21 @@ static int die(const Status &st) {
   return 3;
 }
 
+static int run(int argc, char **argv);
+
+// A device error outside the modes' own handling (e.g. a bad CATEARS_*
+// setting when the runtime starts) ends the driver with a message and exit
+// status 3 instead of std::terminate.
 int main(int argc, char **argv) {
+  try {
+    return run(argc, argv);
+  } catch (const catears::host::DeviceError &e) {
+    fprintf(stderr, "DeviceError: %s\n", e.what());
+    return 3;
+  }
+}
+
+static int run(int argc, char **argv) {
   if (argc < 2) return 1;
   const std::string mode = argv[1];
   if (mode == "fbank" && argc == 5) {

@@ -107,9 +107,10 @@ def test_compat_container_layer(tmp_path):
 
 # ------------------------------------------------------------ GPU checks --
 
-def _run(*args):
+def _run(*args, env=None):
     assert os.path.exists(DRIVER), "pk_dropin not built"
-    r = subprocess.run([DRIVER] + [str(a) for a in args], capture_output=True, text=True, timeout=300)
+    r = subprocess.run([DRIVER] + [str(a) for a in args], capture_output=True, text=True, timeout=300,
+                       env=None if env is None else {**os.environ, **env})
     assert r.returncode == 0, (args[0], r.returncode, r.stderr[-2000:])
 
 
@@ -137,6 +138,26 @@ def test_fbank_streaming_matches_oracle(tmp_path, oracle, chunk):
     assert np.max(np.abs(got - want)) <= FEAT_TOL
     kaldi = np.loadtxt(os.path.join(GOLDEN, "fbankmat_en-us-hello.wav.txt"), dtype=np.float32).reshape(-1, 40)
     assert np.max(np.abs(got - kaldi)) <= 1e-4  # the reference's own bar (test/fbank_test.cc)
+
+
+@pytest.mark.gpu
+def test_fbank_fast_mode_through_the_dropin(tmp_path, oracle):
+    """CATEARS_FBANK=fast selects the four-step-FFT kernel for every lane of
+    the drop-in runtime: streaming Fbank::Process output within the north
+    star's fbank tolerance of the oracle and the Kaldi dump; an unknown value
+    is refused (DeviceError, nonzero exit)."""
+    wave = oracle.read_wav(os.path.join(GOLDEN, "en-us-hello.wav"))
+    out = tmp_path / "f.bin"
+    _run("fbank", _put(tmp_path, "pcm.f32", wave), 777, out, env={"CATEARS_FBANK": "fast"})
+    got = _load(out)
+    want = oracle.Fbank().compute(wave)
+    assert got.shape == want.shape
+    assert 0 < np.max(np.abs(got - want)) <= 1e-4  # the fast kernel, not bit-identical to the exact one
+    kaldi = np.loadtxt(os.path.join(GOLDEN, "fbankmat_en-us-hello.wav.txt"), dtype=np.float32).reshape(-1, 40)
+    assert np.max(np.abs(got - kaldi)) <= 1e-4
+    r = subprocess.run([DRIVER, "fbank", str(tmp_path / "pcm.f32"), "777", str(out)], capture_output=True,
+                       text=True, timeout=300, env={**os.environ, "CATEARS_FBANK": "approximate"})
+    assert r.returncode != 0 and "CATEARS_FBANK" in (r.stdout + r.stderr)
 
 
 @pytest.mark.gpu
