@@ -93,7 +93,7 @@ $(PKLIB): $(PKOBJS) $(LIB)
 	    -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,/opt/rocm/lib -Wl,--no-undefined
 
 $(PKTEST): tests/native/pk_dropin.cc $(PKLIB) $(PKHDRS)
-	$(CXX) $(PKFLAGS) -o $@ $< -Lcatears_amd/lib -lcatears_pk -lcatears_hip -L/opt/rocm/lib -lamdhip64 \
+	$(CXX) $(PKFLAGS) -rdynamic -o $@ $< -Lcatears_amd/lib -lcatears_pk -lcatears_hip -L/opt/rocm/lib -lamdhip64 \
 	    -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,/opt/rocm/lib
 
 COMPATTEST := build/bin/compat_test

@@ -88,8 +88,20 @@ struct FbankTables {
   // frame; not the reference's operation order, <= 3e-5 on log-mel)
   float ff_tw[16 * 16 * 2];         // W256^(n2 k1) = (cos, -sin)(2 pi n2 k1 / 256) at [k1][n2]
   float ff_post[kHalf * 2];         // W512^k = (cos, -sin)(2 pi k / 512), k = 0..255
-  int ff_lane_band[16 * 4];         // mel bands formed by each of a frame's 16 lanes (-1: none)
+  // mel in three slots (kFfSlot): lane j of a frame forms band ff_slot_band[q
+  // * 16 + j] of slot q (-1: none) over a fixed window of kFfSlot[q] bins
+  // starting at ff_slot_start[...] (kept inside 0..255), weights zero outside
+  // the band -- fixed trip counts, so the kernel's dots are straight-line code
+  int ff_slot_band[3 * 16];
+  int ff_slot_start[3 * 16];
+  float ff_slot_w[16 * 52];  // lane j's windows back to back at j * kFfSlotW
 };
+
+// fast-mode mel slot windows (bins): the 16 longest bands (<= 31 bins), the
+// next 16 (<= 12), the last 8 (<= 5); multiples of 4 for 16-byte weight reads
+constexpr int kFfSlot[3] = {32, 12, 8};
+constexpr int kFfSlotBase[3] = {0, 32, 44};
+constexpr int kFfSlotW = 52;
 
 // Builds the tables (tables.cc).
 void build_fbank_tables(FbankTables *t);

@@ -21,9 +21,10 @@
 //      over n2: lane j now holds Z[j + 16 k2];
 //   4. the real-FFT post-pass pairs Z[k] with Z[256 - k] (read back through
 //      LDS) and forms the power spectrum (src/fbank.cc:193-211);
-//   5. mel: each lane forms the 2-3 triangles assigned to it on the host
-//      (balanced by weight count) as float dots over the power spectrum in
-//      LDS (src/fbank.cc:165-184), floor at FLT_EPSILON, logf (:243-244).
+//   5. mel: each lane forms up to three triangles, one per slot (the 16
+//      longest bands, the next 16, the last 8), as float dots over fixed
+//      zero-padded windows of the power spectrum in LDS (src/fbank.cc:165-184),
+//      floor at FLT_EPSILON, logf (:243-244).
 // Twiddles are tabled on the host in double, rounded once.  Error against the
 // oracle: the FFT's own fp32 rounding, measured <= 3e-5 on log-mel (tests).
 #include <float.h>
@@ -46,9 +47,7 @@ struct FastSmem {
   float2 tw[256];       // [k1][n2]
   float2 post[kHalf];
   float window[kWinLen];
-  float mel_w[512];
-  int band[16 * 4];
-  int mel_off[kMel], mel_len[kMel], mel_wbase[kMel];
+  float mel_w[16 * kFfSlotW];  // FbankTables::ff_slot_w
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -133,17 +132,17 @@ __global__ __launch_bounds__(kWaves * 64, 3) void fbank_fast_kernel(const FbankT
   for (int i = threadIdx.x; i < kHalf; i += blockDim.x)
     sm.post[i] = make_float2(tab->ff_post[2 * i], tab->ff_post[2 * i + 1]);
   for (int i = threadIdx.x; i < kWinLen; i += blockDim.x) sm.window[i] = tab->window[i];
-  for (int i = threadIdx.x; i < 512; i += blockDim.x) sm.mel_w[i] = tab->mel_w[i];
-  for (int i = threadIdx.x; i < 64; i += blockDim.x) sm.band[i] = tab->ff_lane_band[i];
-  for (int i = threadIdx.x; i < kMel; i += blockDim.x) {
-    sm.mel_off[i] = tab->mel_off[i];
-    sm.mel_len[i] = tab->mel_len[i];
-    sm.mel_wbase[i] = tab->mel_wbase[i];
-  }
+  for (int i = threadIdx.x; i < 16 * kFfSlotW; i += blockDim.x) sm.mel_w[i] = tab->ff_slot_w[i];
   __syncthreads();
 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int g = lane >> 4, j = lane & 15;
+  int band[3], start[3];  // this lane's mel slots (tables.cc build_fast)
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    band[q] = tab->ff_slot_band[q * 16 + j];
+    start[q] = tab->ff_slot_start[q * 16 + j];
+  }
   float2 *R = sm.frame[wave] + g * kRegion;  // this frame's LDS region
   // the power spectrum reuses the region, 16 dwords in for odd frames: the
   // regions are 544 dwords apart (= 0 mod 32), so frames 2i and 2i+1 -- one
@@ -234,15 +233,26 @@ __global__ __launch_bounds__(kWaves * 64, 3) void fbank_fast_kernel(const FbankT
 #pragma unroll
     for (int k2 = 0; k2 < 16; ++k2) P[j + 16 * k2] = pw[k2];
     wave_sync();
-    // 5. this lane's mel triangles, floor, log
+    // 5. this lane's mel triangles (one per slot), floor, log.  Fixed
+    // windows: every LDS read of a slot issues before its first product (a
+    // loop over the band's own length waited on each read); the zero weights
+    // around the band add exact zeros, so each dot is the band's own
+    // in-order sum.
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int b = sm.band[j * 4 + q];
-      if (b < 0) continue;
-      const int off = sm.mel_off[b], len = sm.mel_len[b], wb = sm.mel_wbase[b];
+    for (int q = 0; q < 3; ++q) {
+      const float *w = sm.mel_w + j * kFfSlotW + kFfSlotBase[q];
+      const float *pq = P + start[q];
       float e = 0.0f;
-      for (int i = 0; i < len; ++i) e += sm.mel_w[wb + i] * P[off + i];
-      if (active) {
+#pragma unroll
+      for (int i = 0; i < kFfSlot[q]; i += 4) {
+        const float4 w4 = *reinterpret_cast<const float4 *>(w + i);
+        e += w4.x * pq[i];
+        e += w4.y * pq[i + 1];
+        e += w4.z * pq[i + 2];
+        e += w4.w * pq[i + 3];
+      }
+      const int b = band[q];
+      if (active && b >= 0) {
         if (mel_out) mel_out[f * kMel + b] = e;
         feats[f * kMel + b] = logf(e < FLT_EPSILON ? FLT_EPSILON : e);
       }

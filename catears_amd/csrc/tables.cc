@@ -182,9 +182,8 @@ void build_fft_lanes(FbankTables *t) {
 }
 
 // Fast-mode tables: the four-step FFT's inter-pass twiddles, the real-FFT
-// post twiddles (both in double, rounded once) and a balanced assignment of
-// the 40 mel bands to the 16 lanes of a frame (longest band first onto the
-// least-loaded lane, by weight count).
+// post twiddles (both in double, rounded once) and the 40 mel bands in three
+// fixed-size slots of a frame's 16 lanes (zero-padded weight windows).
 void build_fast(FbankTables *t) {
   const double tau = 6.283185307179586476925286766559005;
   for (int k1 = 0; k1 < 16; ++k1)
@@ -198,19 +197,22 @@ void build_fast(FbankTables *t) {
     t->ff_post[2 * k] = (float)cos(a);
     t->ff_post[2 * k + 1] = (float)-sin(a);
   }
-  int load[16] = {0}, count[16] = {0};
-  for (int i = 0; i < 16 * 4; ++i) t->ff_lane_band[i] = -1;
+  // bands by length, longest first: ranks 0-15 fill slot 0, 16-31 slot 1,
+  // 32-39 slot 2 (lane = rank mod 16)
   std::vector<int> order(kMel);
   for (int b = 0; b < kMel; ++b) order[b] = b;
   std::sort(order.begin(), order.end(), [&](int a, int b) {
     return t->mel_len[a] != t->mel_len[b] ? t->mel_len[a] > t->mel_len[b] : a < b;
   });
-  for (int b : order) {
-    int best = -1;
-    for (int l = 0; l < 16; ++l)
-      if (count[l] < 4 && (best < 0 || load[l] < load[best])) best = l;
-    t->ff_lane_band[best * 4 + count[best]++] = b;
-    load[best] += t->mel_len[b];
+  for (int i = 0; i < 3 * 16; ++i) t->ff_slot_band[i] = -1, t->ff_slot_start[i] = 0;
+  for (int r = 0; r < kMel; ++r) {
+    const int q = r / 16, j = r % 16, b = order[r], bound = kFfSlot[q];
+    if (t->mel_len[b] > bound || t->mel_off[b] < 0) abort();  // the geometry is fixed (src/fbank.h)
+    const int start = std::min(t->mel_off[b], kHalf - bound);
+    t->ff_slot_band[q * 16 + j] = b;
+    t->ff_slot_start[q * 16 + j] = start;
+    float *w = t->ff_slot_w + j * kFfSlotW + kFfSlotBase[q] + (t->mel_off[b] - start);
+    for (int i = 0; i < t->mel_len[b]; ++i) w[i] = t->mel_w[t->mel_wbase[b] + i];
   }
 }
 

@@ -33,11 +33,6 @@ class DeviceError : public std::runtime_error {
 // Throws DeviceError("<what>: <ce_gpu_last_error()>") unless rc == CE_GPU_OK.
 void Check(int rc, const char *what);
 
-// Test support: the next `n` Check() calls throw DeviceError as if their
-// device call had failed (exercises the error paths, e.g. the AcousticModel
-// batcher releasing its followers).  Process-wide, thread-safe.
-void InjectDeviceFailures(int n);
-
 // Grow-only device allocation.
 class DeviceBuffer {
  public:

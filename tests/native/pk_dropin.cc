@@ -22,6 +22,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <string>
 #include <thread>
 #include <vector>
@@ -33,6 +34,17 @@
 #include "fbank.h"
 #include "matrix.h"
 #include "nnet.h"
+
+// The drop-in's test hook (runtime.cc declares it weak; product binaries
+// leave it undefined): the next g_inject_failures Check() calls throw
+// DeviceError as if their device call had failed.
+static std::atomic<int> g_inject_failures{0};
+extern "C" int catears_test_inject_failure(void) {
+  int left = g_inject_failures.load();
+  while (left > 0 && !g_inject_failures.compare_exchange_weak(left, left - 1)) {
+  }
+  return left > 0;
+}
 
 using namespace pocketkaldi;
 
@@ -165,7 +177,7 @@ static int run(int argc, char **argv) {
     const int streams = (argc - 4) / 2;
     std::vector<std::thread> threads;
     std::vector<int> failed(streams, 0);
-    if (mode == "am_mt_fail") catears::host::InjectDeviceFailures(1);
+    if (mode == "am_mt_fail") g_inject_failures.store(1);
     for (int i = 0; i < streams; ++i) {
       threads.emplace_back([&, i]() {
        try {
