@@ -82,6 +82,11 @@ def parse():
     ap.add_argument("--c4-dump", default=None,
                     help="c4, tests only: rank 0 writes every gathered row (and its own) per utterance "
                          "to this .npz (small corpora)")
+    ap.add_argument("--fold-all", action="store_true",
+                    help="c3, tests only: fold every row of every step (warm-up included) into the checksum "
+                         "on the stream that scored it -- what rank 0's gather folds at N > 1")
+    ap.add_argument("--as-rank", type=int, default=None,
+                    help="c3, tests only: use this rank's PCM pool (one process reproducing one rank)")
     ap.add_argument("--fbank", choices=["exact", "fast"], default="exact",
                     help="fbank kernel (ce_gpu_ctx_set_fbank): exact = the reference's operation order "
                          "(bit-exact pre-log mel), fast = four-step FFT within 3e-5 on log-mel")
@@ -685,7 +690,8 @@ def main():
 
     # resident PCM pool (distinct utterances per rank)
     pool = max(args.pool, U)
-    pcm_np = np.stack([synth.pcm(rank * 100003 + i, n_samp) for i in range(pool)])
+    seed_rank = rank if args.as_rank is None else args.as_rank
+    pcm_np = np.stack([synth.pcm(seed_rank * 100003 + i, n_samp) for i in range(pool)])
     pcm = torch.from_numpy(pcm_np.astype(np.int16) if args.pcm == "s16" else pcm_np).cuda()
     gstats = None if args.no_cmvn else torch.from_numpy(synth.cmvn_stats_synthetic()).cuda()
     # feature slots: NB being scored plus NB + 2 already featurised, so the
@@ -712,6 +718,7 @@ def main():
         gat = RowGather(counts, model.num_pdfs, torch.float32, "cuda", depth=nbuf)
     comm = torch.cuda.Stream() if gather else None
     checksum = torch.zeros((), dtype=torch.float64, device="cuda")
+    fold = [torch.zeros((), dtype=torch.float64, device="cuda") for _ in backs] if args.fold_all else None
 
     def front_stage(i):
         slot = i % F
@@ -737,6 +744,9 @@ def main():
         stream.wait_event(ready[slot])
         gpu.am_forward(ctxs[b], model, plan, norm[slot], outs[o])
         free[slot].record(stream)
+        if fold is not None:
+            with torch.cuda.stream(stream):
+                fold[b] += outs[o].double().sum()
         ev = torch.cuda.Event()
         ev.record(stream)
         done[o] = ev
@@ -779,6 +789,8 @@ def main():
     # the outputs are consumed (checksum) so no work can be elided
     if gat is not None:
         checksum += gat.checksum
+    elif fold is not None:
+        checksum += sum(fold)
     else:
         checksum += outs[(args.warmup + args.steps - 1) % nbuf].double().sum()
     finite = bool(torch.isfinite(outs[0]).all().item())

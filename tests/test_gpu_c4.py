@@ -65,3 +65,38 @@ def test_c4_two_ranks_bit_identical_to_one_process(tmp_path):
         assert np.array_equal(a[k].view(np.uint32), b[k].view(np.uint32)), k
     # the checksums fold every row of every utterance: equal up to fp64 order
     assert two["checksum"] == pytest.approx(one["checksum"], rel=1e-12)
+
+
+def _bench_c3(extra, nproc):
+    env = dict(os.environ, PYTHONPATH=ROOT, CATEARS_BENCH_DEVICE="0")
+    args = ["bench.py", "--model", "tdnn-xs", "--steps", "6", "--warmup", "2", "--pool", "8",
+            "--no-cpu-baseline"] + extra
+    if nproc > 1:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(nproc),
+               "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args + ["--gpus", str(nproc),
+                                                                                     "--dist-backend", "gloo"]
+    else:
+        cmd = [sys.executable] + args
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(line) == 1, r.stdout[-2000:]
+    return json.loads(line[0])
+
+
+def test_c3_two_ranks_gather_every_row(tmp_path):
+    """The driver's N > 1 C3 command (bench.py main: three nnet streams,
+    per-batch events, the comm stream, RowGather's receive ring and
+    wait_slot), rehearsed with 2 gloo ranks on device 0: rank 0 folds every
+    row of every batch of both ranks, warm-up included.  The same batches
+    scored by one process per rank's PCM pool (--as-rank, --fold-all: every
+    row folded on the stream that scored it) must give the same float64 sum,
+    so no batch is lost, duplicated or read before it is written."""
+    two = _bench_c3([], 2)
+    assert two["n_gpus"] == 2 and two["config"]["gather"] and two["finite"]
+    alone = [_bench_c3(["--fold-all", "--as-rank", str(r)], 1) for r in range(2)]
+    assert all(a["config"]["gather"] is False for a in alone)
+    assert two["checksum"] == pytest.approx(alone[0]["checksum"] + alone[1]["checksum"], rel=1e-12)
+    # the two ranks score different audio: a gather that dropped the peer's
+    # rows (or sent rank 0's twice) would miss by a whole rank's sum
+    assert abs(alone[0]["checksum"] - alone[1]["checksum"]) > 1e-6 * abs(alone[0]["checksum"])
