@@ -1392,9 +1392,13 @@ static int run_steps_i8(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, 
   int max_ldq = 16;
   for (const Step &st : m->steps)
     if (st.is_gemm) max_ldq = std::max(max_ldq, st.i8.spliced ? st.i8.kpad : st.i8.in_width);
+  int max_n = 1;
+  for (const Step &st : m->steps)
+    if (st.is_gemm) max_n = std::max(max_n, st.i8.n);
   const size_t q_bytes = ((size_t)rows * max_ldq + 255) / 256 * 256;
   const size_t rs_bytes = ((size_t)rows * 4 + 255) / 256 * 256;
-  CE_TRY(ensure_scratch(ctx, q_bytes + rs_bytes + 256 + i8_params_scratch_bytes()));
+  const size_t part_bytes = std::max(i8_params_scratch_bytes(), sizeof(float) * 2 * i8_gemm_parts(rows, max_n));
+  CE_TRY(ensure_scratch(ctx, q_bytes + rs_bytes + 256 + part_bytes));
   char *base = static_cast<char *>(ctx->scratch.ptr);
   int8_t *xq = reinterpret_cast<int8_t *>(base);
   int32_t *rowsum = reinterpret_cast<int32_t *>(base + q_bytes);
@@ -1402,15 +1406,20 @@ static int run_steps_i8(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, 
   void *part = base + q_bytes + rs_bytes + 256;
   int cur = 0;
   bool first = true;
-  for (const Step &st : m->steps) {
+  int fused_parts = 0;  // > 0: the previous GEMM left this layer's min / max partials in `part`
+  for (size_t si = 0; si < m->steps.size(); ++si) {
+    const Step &st = m->steps[si];
     if (st.is_gemm) {
       const I8Layer &L = st.i8;
       const int *rm = first ? row_map : nullptr;
       const int ldq = L.spliced ? L.kpad : L.in_width;
       {
         ProfScope prof(ctx, CE_GPU_PROF_QUANT);
-        CE_TRY(launch_i8_params(ctx->stream, x, ldx, rows, L.in_width, rm, row_edge, L.in_left, L.in_right,
-                                part, params));
+        if (fused_parts > 0)
+          CE_TRY(launch_i8_params_fold(ctx->stream, part, fused_parts, params));
+        else
+          CE_TRY(launch_i8_params(ctx->stream, x, ldx, rows, L.in_width, rm, row_edge, L.in_left, L.in_right,
+                                  part, params));
         if (L.spliced) {
           CE_TRY(launch_i8_quantize(ctx->stream, x, ldx, rows, L.in_width, rm, st.gemm.nseg, st.gemm.off, params,
                                     xq, ldq, rowsum));
@@ -1419,13 +1428,25 @@ static int run_steps_i8(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, 
           CE_TRY(launch_i8_quantize(ctx->stream, x, ldx, rows, L.in_width, rm, 1, zero, params, xq, ldq, rowsum));
         }
       }
+      // the next step reads this GEMM's output directly: its min / max is
+      // reduced in this GEMM's epilogue (the partials are read by the next
+      // layer's fold before the next GEMM overwrites them: stream order)
+      const bool fuse = si + 1 < m->steps.size() && m->steps[si + 1].is_gemm && m->steps[si + 1].i8.in_width == L.n;
+      I8NextMinMax mm = {};
+      if (fuse) {
+        const I8Layer &N = m->steps[si + 1].i8;
+        mm = I8NextMinMax{part, row_edge, N.in_left, N.in_right};
+      }
+      fused_parts = 0;
       ProfScope prof(ctx, CE_GPU_PROF_GEMM);
-      CE_TRY(launch_i8_gemm(ctx->stream, L, xq, ldq, rows, rowsum, params, buf[cur], L.n));
+      CE_TRY(launch_i8_gemm(ctx->stream, L, xq, ldq, rows, rowsum, params, buf[cur], L.n, fuse ? &mm : nullptr,
+                            fuse ? &fused_parts : nullptr));
       x = buf[cur];
       ldx = L.n;
       cur ^= 1;
       first = false;
     } else {
+      fused_parts = 0;
       CE_TRY(launch_rowop(ctx->stream, st.row, const_cast<float *>(x), ldx, rows));
     }
   }

@@ -189,6 +189,19 @@ __device__ __forceinline__ void with_post_mode(int mode, F &&f) {
   }
 }
 
+// The same, returning f's result.
+template <class F>
+__device__ __forceinline__ auto with_post_mode_r(int mode, F &&f) {
+  switch (mode) {
+    case kPostModeNone: return f(std::integral_constant<int, kPostModeNone>());
+    case kPostModeRelu: return f(std::integral_constant<int, kPostModeRelu>());
+    case kPostModeBn: return f(std::integral_constant<int, kPostModeBn>());
+    case kPostModeReluBn: return f(std::integral_constant<int, kPostModeReluBn>());
+    case kPostModeBnRelu: return f(std::integral_constant<int, kPostModeBnRelu>());
+    default: return f(std::integral_constant<int, kPostModeGeneric>());
+  }
+}
+
 struct GemmLayer {
   int din = 0;            // input row width (one splice segment)
   int nseg = 1;           // splice indices (segments of the K dimension)
@@ -500,8 +513,19 @@ int launch_i8_params(hipStream_t s, const float *x, int ldx, int rows, int width
 size_t i8_params_scratch_bytes();
 int launch_i8_quantize(hipStream_t s, const float *x, int ldx, int rows, int width, const int *row_map, int nseg,
                        const int *offs, const void *params, int8_t *q, int ldq, int32_t *rowsum);
+// The next layer's min / max, fused into this GEMM's epilogue: one float2
+// per wave into `part` (at least i8_gemm_parts(m, n)), over the rows the
+// next layer holds (as launch_i8_params); launch_i8_params_fold then forms
+// that layer's parameters from the *nparts partials.
+struct I8NextMinMax {
+  void *part;
+  const uint32_t *row_edge;
+  int in_left, in_right;
+};
 int launch_i8_gemm(hipStream_t s, const I8Layer &L, const int8_t *a, int lda, int m, const int32_t *rowsum,
-                   const void *pa, float *y, int ldy);
+                   const void *pa, float *y, int ldy, const I8NextMinMax *mm = nullptr, int *nparts = nullptr);
+int launch_i8_params_fold(hipStream_t s, const void *part, int nparts, void *params);
+size_t i8_gemm_parts(int m, int n);
 int i8_k_align();
 int launch_gemm_u8_ws(hipStream_t s, int m, int n, int k, const uint8_t *a, const void *pa,
                       const uint8_t *b, const void *pb, float *c_f32, int32_t *c_i32, void *ws);

@@ -214,7 +214,53 @@ struct I8Args {
   int ldy;
   int tiles_n, tiles_m, group;
   int vec_epi;              // i8_epilogue_v (16-byte row stores)
+  // Non-null: the epilogue also reduces the (min, max) of its outputs over the
+  // rows the NEXT layer's Quantize reads (minmax_kernel's held-row rule with
+  // that layer's in_left / in_right) into mm_part[blockIdx.x], so the next
+  // layer's parameters fold these partials instead of re-reading the output.
+  float2 *mm_part;
+  const uint32_t *row_edge;
+  int mm_left, mm_right;
 };
+
+// p.off[seg] through a select chain: a runtime index into the kernel
+// argument's array can force the whole argument struct into scratch memory
+// (the readfirstlane keeps the compiler from turning the chain back into a
+// load from a selected address)
+__device__ __forceinline__ int seg_off(const I8Args &p, int seg) {
+  int v = __builtin_amdgcn_readfirstlane(p.off[0]);
+#pragma unroll
+  for (int i = 1; i < 8; ++i) v = seg >= i ? __builtin_amdgcn_readfirstlane(p.off[i]) : v;
+  return v;
+}
+
+// minmax_kernel's row rule: does the next layer's Quantize count row `row`?
+__device__ __forceinline__ uint32_t mm_held(const uint32_t *row_edge, int m, int left, int right, int row) {
+  if (row >= m) return 0;
+  const int dl = row_edge ? (int)(row_edge[row] & 0xffff) : row;
+  const int dr = row_edge ? (int)(row_edge[row] >> 16) : m - 1 - row;
+  return dl >= left && dr >= right;
+}
+
+// FindMinMax's comparisons (matrix.cc:337-342: NaN never wins one)
+__device__ __forceinline__ void mm_take(float y, float &mn, float &mx) {
+  if (y > mx) mx = y;
+  if (y < mn) mn = y;
+}
+
+// Wave (min, max) of the epilogue's held outputs -> part[blockIdx.x * NW +
+// wave] (no block barrier: a barrier under the epilogue's runtime `mm` test
+// made the compiler copy the whole argument struct to scratch memory).
+template <int NT>
+__device__ __forceinline__ void mm_store(float2 *part, float mn, float mx) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const float omn = __shfl_xor(mn, d, 64), omx = __shfl_xor(mx, d, 64);
+    mn = omn < mn ? omn : mn;
+    mx = omx > mx ? omx : mx;
+  }
+  if ((threadIdx.x & 63) == 0) part[blockIdx.x * (NT / 64) + (threadIdx.x >> 6)] = make_float2(mn, mx);
+}
 
 // Zero-point restore + bias + ReLU / BatchNorm + store of one wave's
 // (TI x 32) x (TJ x 32) accumulator tile at (m0 + wrow, col0).  Column
@@ -245,9 +291,12 @@ __device__ __forceinline__ void i8_epilogue(const I8Args &p, const i32x16 (&acc)
       }
     }
     srs[t] = cb * sum;
+    if (p.mm_part) srs[BM + t] = mm_held(p.row_edge, p.m, p.mm_left, p.mm_right, row);
   }
   __syncthreads();
-  with_post_mode(p.post_mode, [&](auto M) {
+  const bool mm = p.mm_part != nullptr;
+  const float2 mm2 = with_post_mode_r(p.post_mode, [&](auto M) {
+    float mn = FLT_MAX, mx = FLT_MIN;  // matrix.cc:335-336
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       const int col = col0 + j * 32 + r;
@@ -265,11 +314,14 @@ __device__ __forceinline__ void i8_epilogue(const I8Args &p, const i32x16 (&acc)
           float y = (float)(int32_t)v * cscale;
           y = y + bias;  // +0 when absent: y is never -0 here (int * positive scale)
           y = apply_post<decltype(M)::value>(y, sc, of, p.post, p.npost);
+          if (mm && srs[BM + lr]) mm_take(y, mn, mx);
           if (m0 + lr < p.m) p.y[(int64_t)(m0 + lr) * p.ldy + col] = y;
         }
       }
     }
+    return make_float2(mn, mx);
   });
+  if (mm) mm_store<NT>(p.mm_part, mm2.x, mm2.y);
 }
 
 // The same epilogue with the stores vectorised: each wave finishes its tile
@@ -306,7 +358,14 @@ __device__ __forceinline__ void i8_epilogue_v(const I8Args &p, const i32x16 (&ac
     srs[t] = cb * sum;
   }
   __syncthreads();
-  // column constants of this lane's TJ columns, loaded once
+  // the next layer's held rows among this wave's 64: bit t = row wrow + t
+  static_assert(TI == 2, "one 64-row mask per wave");
+  const bool mm = p.mm_part != nullptr;
+  const uint64_t hmask =
+      mm ? __builtin_amdgcn_ballot_w64(mm_held(p.row_edge, p.m, p.mm_left, p.mm_right, m0 + wrow + lane)) : 0;
+  // column constants of this lane's TJ columns, loaded once (columns past n
+  // take column n-1's, and so do their weight rows in the caller's B loader:
+  // such lanes repeat a valid output, which cannot move a min or max)
   uint32_t cterm[TJ];
   float bias[TJ], sc[TJ], of[TJ];
 #pragma unroll
@@ -318,9 +377,15 @@ __device__ __forceinline__ void i8_epilogue_v(const I8Args &p, const i32x16 (&ac
     of[j] = p.bn_offset ? p.bn_offset[col] : 0.0f;
   }
   constexpr int C4 = TJ * 8;  // float4 chunks per slab row
-  with_post_mode(p.post_mode, [&](auto M) {
+  const float2 mm2 = with_post_mode_r(p.post_mode, [&](auto M) {
+    // FindMinMax (matrix.cc:331-345) as max / min: NaN never wins either way,
+    // and a zero's sign cannot change the parameters
+    float mn = FLT_MAX, mx = FLT_MIN;  // matrix.cc:335-336
 #pragma unroll
     for (int i = 0; i < TI; ++i) {
+      float rmn[16], rmx[16];  // per row of the lane, over its TJ columns
+#pragma unroll
+      for (int e = 0; e < 16; ++e) rmn[e] = FLT_MAX, rmx[e] = FLT_MIN;
 #pragma unroll
       for (int j = 0; j < TJ; ++j)
 #pragma unroll
@@ -329,8 +394,19 @@ __device__ __forceinline__ void i8_epilogue_v(const I8Args &p, const i32x16 (&ac
           const uint32_t v = (uint32_t)acc[i][j][e] + srs[wrow + i * 32 + rr] + cterm[j];
           float y = (float)(int32_t)v * cscale;
           y = y + bias[j];  // +0 when absent: y is never -0 here (int * positive scale)
-          slab[rr * SW + j * 32 + r] = apply_post<decltype(M)::value>(y, sc[j], of[j], p.post, p.npost);
+          y = apply_post<decltype(M)::value>(y, sc[j], of[j], p.post, p.npost);
+          rmx[e] = fmaxf(rmx[e], y);
+          rmn[e] = fminf(rmn[e], y);
+          slab[rr * SW + j * 32 + r] = y;
         }
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int rr = (e & 3) + 8 * (e >> 2) + 4 * h;
+        if ((hmask >> (i * 32 + rr)) & 1) {
+          mx = fmaxf(mx, rmx[e]);
+          mn = fminf(mn, rmn[e]);
+        }
+      }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -345,7 +421,9 @@ __device__ __forceinline__ void i8_epilogue_v(const I8Args &p, const i32x16 (&ac
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    return make_float2(mn, mx);
   });
+  if (mm) mm_store<NT>(p.mm_part, mm2.x, mm2.y);
 }
 
 __global__ __launch_bounds__(256, 2) void gemm_i8_nnet_kernel(I8Args p) {
@@ -367,7 +445,7 @@ __global__ __launch_bounds__(256, 2) void gemm_i8_nnet_kernel(I8Args p) {
   for (int k0 = 0; k0 < p.kpad; k0 += IBK) {
     // one K-tile never straddles a segment (din % 64 == 0 or nseg == 1)
     const int seg = k0 / p.din, col0 = k0 - seg * p.din;
-    const int shift = p.off[seg < 8 ? seg : 7];
+    const int shift = seg_off(p, seg);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int idx = tid + 256 * i, row = idx >> 2, c16 = idx & 3;
@@ -454,7 +532,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_i8_glds_kernel(I8Args 
     const int seg = k0 / p.din, col0 = k0 - seg * p.din;
     if (seg != cur_seg) {
       cur_seg = seg;
-      const int shift = p.off[seg < 8 ? seg : 7];
+      const int shift = seg_off(p, seg);
 #pragma unroll
       for (int i = 0; i < NGA; ++i) {
         const int row = (wave * NGA + i) * RPI + lrow;
@@ -541,7 +619,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_i8_glds_kernel(I8Args 
     p.y[(int64_t)blockIdx.x * 64 * NW + tid] = (float)t;
     return;
   }
-  constexpr bool kVecFits = NW * 32 * (TJ * 32 + 8) * 4 + BM * 4 <= STAGES * STAGE;  // slabs in the stages
+  constexpr bool kVecFits = NW * 32 * (TJ * 32 + 8) * 4 + BM * 4 <= STAGES * STAGE;  // slabs + row sums
   if (kVecFits && p.vec_epi)
     i8_epilogue_v<TI, TJ, BM, 64 * NW>(p, acc, m0, wm * TI * 32, n0 + wn * TJ * 32, r, h,
                                        reinterpret_cast<char *>(smem));
@@ -597,7 +675,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_i8_q_kernel(I8Args p) 
     kt = min(kt, ktiles - 1);
     const int k0 = kt * BKB;
     const int seg = k0 / p.din, col0 = k0 - seg * p.din;
-    const int shift = p.off[seg < 8 ? seg : 7];
+    const int shift = seg_off(p, seg);
     int8_t *st = smem + (kt % 3) * STAGE;
     const char *abase = reinterpret_cast<const char *>(p.a) + col0;
     const char *bbase = reinterpret_cast<const char *>(p.w) + k0;
@@ -707,7 +785,7 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_i8_reg_kernel(I8Args p
     const int seg = k0 / p.din, col0 = k0 - seg * p.din;
     if (seg != cur_seg) {
       cur_seg = seg;
-      const int shift = p.off[seg < 8 ? seg : 7];
+      const int shift = seg_off(p, seg);
 #pragma unroll
       for (int i = 0; i < LA; ++i) {
         int src = m0 + row_base + i * RSTEP + shift;
@@ -795,9 +873,22 @@ int launch_i8_quantize(hipStream_t s, const float *x, int ldx, int rows, int wid
   return CE_GPU_OK;
 }
 
+int launch_i8_params_fold(hipStream_t s, const void *part, int nparts, void *params) {
+  hipLaunchKernelGGL(params_kernel, dim3(1), dim3(256), 0, s, static_cast<const float2 *>(part), nparts,
+                     static_cast<QP *>(params));
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
 int launch_i8_gemm(hipStream_t s, const I8Layer &L, const int8_t *a, int lda, int m, const int32_t *rowsum,
-                   const void *pa, float *y, int ldy) {
+                   const void *pa, float *y, int ldy, const I8NextMinMax *mm, int *nparts) {
   I8Args p = {};
+  if (mm) {
+    p.mm_part = static_cast<float2 *>(mm->part);
+    p.row_edge = mm->row_edge;
+    p.mm_left = mm->in_left;
+    p.mm_right = mm->in_right;
+  }
   p.a = a;
   p.lda = lda;
   p.m = m;
@@ -835,6 +926,7 @@ int launch_i8_gemm(hipStream_t s, const I8Layer &L, const int8_t *a, int lda, in
       p.tiles_n = (L.n + bn - 1) / bn;
       p.tiles_m = (m + bm - 1) / bm;
       p.group = 8;  // an XCD's tiles: 8 column tiles x its row blocks
+      if (nparts) *nparts = p.tiles_m * p.tiles_n * (threads / 64);  // one partial per wave
       hipLaunchKernelGGL(kern, dim3(p.tiles_m * p.tiles_n), dim3(threads), 0, s, p);
     };
     switch (use_glds) {
@@ -902,11 +994,16 @@ int launch_i8_gemm(hipStream_t s, const I8Layer &L, const int8_t *a, int lda, in
   if (p.kpad % IBK != 0 || (p.nseg > 1 && p.din % IBK != 0) || lda % 16 != 0)
     return fail(CE_GPU_EINVAL, "gemm_i8_nnet: bad K geometry");
   const int tiles_m = (m + IBM - 1) / IBM;
+  if (nparts) *nparts = tiles_m * p.tiles_n * 4;
   hipLaunchKernelGGL(gemm_i8_nnet_kernel, dim3(tiles_m * p.tiles_n), dim3(256), 0, s, p);
   CE_HIP(hipGetLastError());
   return CE_GPU_OK;
 }
 
 int i8_k_align() { return 128; }  // the LDS-DMA kernel's K-tile (bytes)
+
+// one partial per wave; every int8 GEMM tile is at least 128 x 128 with at
+// most 8 waves
+size_t i8_gemm_parts(int m, int n) { return (size_t)((m + 127) / 128) * ((n + 127) / 128) * 8; }
 
 }  // namespace catears
