@@ -64,3 +64,15 @@ def test_product_library_has_no_ablation_kernels():
     lat = re.findall(rb"lat_gemm_kernelILi\d+ELi\d+ELb[01]ELi(\d+)E", data)
     assert lat, "no latency GEMM found"
     assert set(lat) == {b"0"}, sorted(set(lat))
+
+
+def test_dropin_library_defines_no_test_hook():
+    """The drop-in's failure injection is test-only: libcatears_pk.so holds an
+    undefined weak reference to catears_test_inject_failure (null in every
+    product binary) and no definition; only the test driver defines it."""
+    import subprocess
+    pk = os.path.join(ROOT, "catears_amd", "lib", "libcatears_pk.so")
+    out = subprocess.run(["nm", "-D", pk], capture_output=True, text=True, check=True).stdout
+    hook = [ln.split() for ln in out.splitlines() if ln.endswith(" catears_test_inject_failure")]
+    assert hook and all(f[-2] == "w" for f in hook), hook
+    assert "InjectDeviceFailures" not in out
