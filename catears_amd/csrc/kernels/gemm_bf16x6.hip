@@ -1074,7 +1074,15 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
   for (int i = 0; i < 4; ++i) p.post[i] = a.post[i];
   p.npost = a.npost;
   p.post_mode = post_mode(a.post, a.npost);
-  p.group = 8;
+// Column tiles per XCD tile group (tile_order.h).  A hidden layer's 128
+// tiles (32 row x 4 unit) give each XCD 16: group 2 makes that 8 row x 2
+// unit tiles -- 9.5 MB of weight fragments + 12.5 MB of activations into its
+// L2, against 18.9 + 6.3 MB for the whole-width group 8 (C3 at the driver's
+// step counts, alternating builds: 5.53-5.61 vs 5.45-5.52 M frames/s).
+#ifndef CATEARS_X6_GROUP
+#define CATEARS_X6_GROUP 2
+#endif
+  p.group = CATEARS_X6_GROUP;
   p.wd = a.wd;
   p.wd_kt = a.wd_kt;
   const bool out16 = a.y16 != nullptr;
