@@ -13,7 +13,9 @@
 //                        packed buffers keep full height, so the edge rows the
 //                        earlier Narrows dropped (computed from clamped
 //                        indices) are skipped by their distance to the
-//                        segment edges.
+//                        segment edges.  Layers whose input is the previous
+//                        GEMM's output skip minmax_kernel: that GEMM's
+//                        epilogue leaves per-wave partials (I8Args::mm_part).
 //   2. quantize_kernel   q = roundf(clamp(x / scale + zp, 0, 255)) stored as the
 //                        signed byte q ^ 0x80 = q - 128, with the row sums of
 //                        those bytes.  Layers whose segment width is not a
