@@ -74,6 +74,11 @@ def _rows(rank, step, n, width):
     return (1000.0 * rank + 10.0 * step + np.arange(n)[:, None] + 0.001 * np.arange(width)[None, :]).astype(np.float32)
 
 
+# ragged per-rank batch lists: ranks with a step more or fewer than rank 0,
+# steps with no rows, a rank with no rows at all (3)
+_COUNTS = {0: [5, 3, 4], 1: [2, 6, 0, 1], 2: [8, 1, 1, 7, 2], 3: []}
+
+
 def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -82,7 +87,7 @@ def _worker(rank, world, port, q):
         width = 7
         # ragged per-rank batch lists: rank 1 has one step more, and a step
         # with no rows at all
-        mine = {0: [5, 3, 4], 1: [2, 6, 0, 1]}[rank]
+        mine = _COUNTS[rank]
         counts = exchange_counts(mine)
         g = RowGather(counts, width, torch.float32, "cpu", depth=2, keep=True)
         bufs = [torch.empty(8, width) for _ in range(2)]
@@ -102,8 +107,12 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_row_gather_gloo_ragged():
-    world = 2
+@pytest.mark.parametrize("world", [2, 4])
+def test_row_gather_gloo_ragged(world):
+    """RowGather on `world` gloo ranks: with 4, rank 0 posts the receives of
+    three peers in one grouped batch_isend_irecv per step (the N = 4 / 8
+    shape), peers run out of steps at different times and one peer sends
+    nothing."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -117,12 +126,12 @@ def test_row_gather_gloo_ragged():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    counts = {0: [5, 3, 4], 1: [2, 6, 0, 1]}
+    counts = {r: _COUNTS[r] for r in range(world)}
     want = sum(float(_rows(r, s, n, 7).astype(np.float64).sum()) for r in counts for s, n in enumerate(counts[r]) if n)
     assert res[0][0] == pytest.approx(want, rel=1e-12)
-    assert res[0][1] == 2 + 6 + 1
+    assert res[0][1] == sum(sum(counts[r]) for r in counts if r)
     # every received row, full width, exactly the sender's
     got = {(p, s): np.array(a, np.float32) for p, s, a in res[0][2]}
-    assert sorted(got) == [(1, 0), (1, 1), (1, 3)]
+    assert sorted(got) == sorted((p, s) for p in counts if p for s, n in enumerate(counts[p]) if n)
     for (p, s), a in got.items():
         assert np.array_equal(a, _rows(p, s, counts[p][s], 7))
