@@ -82,6 +82,10 @@ def parse():
     ap.add_argument("--c4-dump", default=None,
                     help="c4, tests only: rank 0 writes every gathered row (and its own) per utterance "
                          "to this .npz (small corpora)")
+    ap.add_argument("--host-io", action="store_true",
+                    help="c3: the PCIe-inclusive rate of a host-side caller -- every step's PCM is copied from "
+                         "pinned host memory and its log-likelihoods back to pinned host memory, on copy streams "
+                         "overlapped with the compute (DESIGN.md §6; never the headline value)")
     ap.add_argument("--fold-all", action="store_true",
                     help="c3, tests only: fold every row of every step (warm-up included) into the checksum "
                          "on the stream that scored it -- what rank 0's gather folds at N > 1")
@@ -719,13 +723,34 @@ def main():
     comm = torch.cuda.Stream() if gather else None
     checksum = torch.zeros((), dtype=torch.float64, device="cuda")
     fold = [torch.zeros((), dtype=torch.float64, device="cuda") for _ in backs] if args.fold_all else None
+    # --host-io: a host caller's buffers.  PCM slots on the device are
+    # refilled from pinned host memory on an upload stream; each batch's
+    # log-likelihoods go back to a pinned host ring on a download stream,
+    # and a batch may overwrite outs[o] only once its download has finished.
+    hio = None
+    if args.host_io:
+        host_pcm = pcm.cpu().pin_memory()
+        dev_pcm = [torch.empty((U,) + tuple(pcm.shape[1:]), dtype=pcm.dtype, device="cuda") for _ in range(F)]
+        host_out = [torch.empty(tuple(outs[0].shape), dtype=torch.float32).pin_memory() for _ in range(nbuf)]
+        hio = {"up": torch.cuda.Stream(), "down": torch.cuda.Stream(),
+               "down_done": [None] * nbuf}
 
     def front_stage(i):
         slot = i % F
         front, ctx_f = fronts[i % NF], ctx_fs[i % NF]
         front.wait_event(free[slot])  # the batch F steps ago has finished reading this slot
         first = (i * U) % (pool - U + 1)
-        src = pcm[first:first + U].reshape(-1)
+        if hio is not None:
+            up = hio["up"]
+            up.wait_event(free[slot])  # the fbank F steps ago has read dev_pcm[slot]
+            with torch.cuda.stream(up):
+                dev_pcm[slot].copy_(host_pcm[first:first + U], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(up)
+            front.wait_event(ev)
+            src = dev_pcm[slot].reshape(-1)
+        else:
+            src = pcm[first:first + U].reshape(-1)
         gpu.fbank(ctx_f, plan, src, raw[slot])
         if gstats is not None:
             gpu.cmvn(ctx_f, plan, gstats, raw[slot], norm[slot])
@@ -741,6 +766,8 @@ def main():
                 gat.wait_slot(o)
         if done[o] is not None:
             stream.wait_event(done[o])  # the batch nbuf steps ago (maybe another stream) wrote outs[o]
+        if hio is not None and hio["down_done"][o] is not None:
+            stream.wait_event(hio["down_done"][o])  # ... and its log-likelihoods are on the host
         stream.wait_event(ready[slot])
         gpu.am_forward(ctxs[b], model, plan, norm[slot], outs[o])
         free[slot].record(stream)
@@ -750,6 +777,14 @@ def main():
         ev = torch.cuda.Event()
         ev.record(stream)
         done[o] = ev
+        if hio is not None:
+            down = hio["down"]
+            down.wait_event(ev)
+            with torch.cuda.stream(down):
+                host_out[o].copy_(outs[o], non_blocking=True)
+            dv = torch.cuda.Event()
+            dv.record(down)
+            hio["down_done"][o] = dv
         if gat is not None:
             # the transfer is enqueued from a stream of its own that waits
             # for this batch only, so the nnet streams never wait on each
@@ -940,7 +975,7 @@ def main():
                    "frames_per_step_per_gpu": frames_per_step, "packed_rows": plan.max_chunk_rows,
                    "cmvn": not args.no_cmvn, "fbank": args.fbank, "pcm": args.pcm, "parallelism": f"utterance shard x{world}",
                    "streams": 1 if args.serial else 1 + NB,
-                   "gather": gather},
+                   "gather": gather, "host_io": bool(args.host_io)},
         "roofline": roofline, "cpu_baseline": cpu, "stages": stages,
         "end_to_end_mfma_frac": round(value / world * FLOPS_PER_FRAME / 1e12 /
                                       (MFMA_I8_PEAK_TOPS if int8 else
