@@ -89,6 +89,9 @@ def parse():
     ap.add_argument("--fold-all", action="store_true",
                     help="c3, tests only: fold every row of every step (warm-up included) into the checksum "
                          "on the stream that scored it -- what rank 0's gather folds at N > 1")
+    ap.add_argument("--c3-dump", default=None,
+                    help="c3, tests only: write every step's log-likelihood rows (rank 0: its own and every "
+                         "peer's) to this .npz, copied on the device on the stream that consumes them")
     ap.add_argument("--as-rank", type=int, default=None,
                     help="c3, tests only: use this rank's PCM pool (one process reproducing one rank)")
     ap.add_argument("--fbank", choices=["exact", "fast"], default="exact",
@@ -719,10 +722,12 @@ def main():
     gat = None
     if gather:
         counts = exchange_counts([frames_per_step] * (args.warmup + args.steps))
-        gat = RowGather(counts, model.num_pdfs, torch.float32, "cuda", depth=nbuf)
+        gat = RowGather(counts, model.num_pdfs, torch.float32, "cuda", depth=nbuf,
+                        keep=bool(args.c3_dump) and rank == 0)
     comm = torch.cuda.Stream() if gather else None
     checksum = torch.zeros((), dtype=torch.float64, device="cuda")
     fold = [torch.zeros((), dtype=torch.float64, device="cuda") for _ in backs] if args.fold_all else None
+    dump = {} if args.c3_dump and rank == 0 else None  # step -> device copy of this rank's rows
     # --host-io: a host caller's buffers.  PCM slots on the device are
     # refilled from pinned host memory on an upload stream; each batch's
     # log-likelihoods go back to a pinned host ring on a download stream,
@@ -774,6 +779,11 @@ def main():
         if fold is not None:
             with torch.cuda.stream(stream):
                 fold[b] += outs[o].double().sum()
+                if dump is not None:
+                    dump[i] = outs[o].clone()
+                    if os.environ.get("CATEARS_DUMP_FEATS"):
+                        dump[f"raw{i}"] = raw[slot].clone()
+                        dump[f"norm{i}"] = norm[slot].clone()
         ev = torch.cuda.Event()
         ev.record(stream)
         done[o] = ev
@@ -791,6 +801,8 @@ def main():
             # other through it
             with torch.cuda.stream(comm):
                 comm.wait_event(ev)
+                if dump is not None:
+                    dump[i] = outs[o].clone()
                 assert gat.submit(i, outs[o], own=outs[o] if rank == 0 else None) == o
 
     def run(first, count):
@@ -829,6 +841,12 @@ def main():
     else:
         checksum += outs[(args.warmup + args.steps - 1) % nbuf].double().sum()
     finite = bool(torch.isfinite(outs[0]).all().item())
+    if dump is not None:
+        arrs = {(f"r{seed_rank}s{k}" if isinstance(k, int) else f"r{seed_rank}{k}"): v.cpu().numpy()
+                for k, v in dump.items()}
+        for p, st, a in (gat.keep or []) if gat is not None else []:
+            arrs[f"r{p}s{st}"] = a
+        np.savez(args.c3_dump, **arrs)
     # f16x3: no activation left the two-plane range in any batch
     overflow = any(c.overflow() for c in set(ctxs + ctx_fs))
 
