@@ -90,8 +90,8 @@ def parse():
                     help="c3, tests only: fold every row of every step (warm-up included) into the checksum "
                          "on the stream that scored it -- what rank 0's gather folds at N > 1")
     ap.add_argument("--c3-dump", default=None,
-                    help="c3, tests only: write every step's log-likelihood rows (rank 0: its own and every "
-                         "peer's) to this .npz, copied on the device on the stream that consumes them")
+                    help="c3, tests only: write every step's log-likelihood rows (every rank its own, as "
+                         "sent; rank 0 also every peer's, as received) to this .npz (.rankR.npz at N > 1)")
     ap.add_argument("--as-rank", type=int, default=None,
                     help="c3, tests only: use this rank's PCM pool (one process reproducing one rank)")
     ap.add_argument("--fbank", choices=["exact", "fast"], default="exact",
@@ -727,7 +727,7 @@ def main():
     comm = torch.cuda.Stream() if gather else None
     checksum = torch.zeros((), dtype=torch.float64, device="cuda")
     fold = [torch.zeros((), dtype=torch.float64, device="cuda") for _ in backs] if args.fold_all else None
-    dump = {} if args.c3_dump and rank == 0 else None  # step -> device copy of this rank's rows
+    dump = {} if args.c3_dump else None  # step -> device copy of this rank's rows
     # --host-io: a host caller's buffers.  PCM slots on the device are
     # refilled from pinned host memory on an upload stream; each batch's
     # log-likelihoods go back to a pinned host ring on a download stream,
@@ -846,7 +846,7 @@ def main():
                 for k, v in dump.items()}
         for p, st, a in (gat.keep or []) if gat is not None else []:
             arrs[f"r{p}s{st}"] = a
-        np.savez(args.c3_dump, **arrs)
+        np.savez(args.c3_dump if world == 1 else args.c3_dump.replace(".npz", f".rank{rank}.npz"), **arrs)
     # f16x3: no activation left the two-plane range in any batch
     overflow = any(c.overflow() for c in set(ctxs + ctx_fs))
 

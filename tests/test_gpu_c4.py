@@ -87,16 +87,23 @@ def _bench_c3(extra, nproc):
 def test_c3_two_ranks_gather_every_row(tmp_path):
     """The driver's N > 1 C3 command (bench.py main: three nnet streams,
     per-batch events, the comm stream, RowGather's receive ring and
-    wait_slot), rehearsed with 2 gloo ranks on device 0: rank 0 folds every
-    row of every batch of both ranks, warm-up included.  The same batches
-    scored by one process per rank's PCM pool (--as-rank, --fold-all: every
-    row folded on the stream that scored it) must give the same float64 sum,
-    so no batch is lost, duplicated or read before it is written."""
-    two = _bench_c3([], 2)
+    wait_slot), rehearsed with 2 gloo ranks on device 0.  Within the run:
+    every batch rank 1 sends (its rows as scored, copied on the stream that
+    hands them to the gather) arrives at rank 0 bit for bit, and rank 0's
+    checksum folds exactly its own batches and the received ones, warm-up
+    included -- no batch lost, duplicated or read before it was written."""
+    steps = 6 + 2
+    two = _bench_c3(["--c3-dump", str(tmp_path / "d.npz")], 2)
     assert two["n_gpus"] == 2 and two["config"]["gather"] and two["finite"]
-    alone = [_bench_c3(["--fold-all", "--as-rank", str(r)], 1) for r in range(2)]
-    assert all(a["config"]["gather"] is False for a in alone)
-    assert two["checksum"] == pytest.approx(alone[0]["checksum"] + alone[1]["checksum"], rel=1e-12)
+    r0, r1 = np.load(tmp_path / "d.rank0.npz"), np.load(tmp_path / "d.rank1.npz")
+    assert sorted(r1.files) == sorted(f"r1s{s}" for s in range(steps))
+    want = 0.0
+    for s in range(steps):
+        sent, got, own = r1[f"r1s{s}"], r0[f"r1s{s}"], r0[f"r0s{s}"]
+        assert sent.shape == got.shape == own.shape
+        assert np.array_equal(sent.view(np.uint32), got.view(np.uint32)), s
+        want += float(own.astype(np.float64).sum()) + float(got.astype(np.float64).sum())
+    assert two["checksum"] == pytest.approx(want, rel=1e-12)
     # the two ranks score different audio: a gather that dropped the peer's
     # rows (or sent rank 0's twice) would miss by a whole rank's sum
-    assert abs(alone[0]["checksum"] - alone[1]["checksum"]) > 1e-6 * abs(alone[0]["checksum"])
+    assert not np.array_equal(r0["r0s0"], r0["r1s0"])
