@@ -47,6 +47,11 @@ $(OBJ)/gemm_bf16x6.o $(OBJ)/gemm_f16x3.o: HIPFLAGS += -mllvm -disable-promote-al
 # VALU costs more issue cycles than the scalar pair in an MFMA gap)
 $(OBJ)/gemm_bf16x6.o: HIPFLAGS += -fno-slp-vectorize $(X6FLAGS)
 
+# the exact fbank kernel holds a frame's FFT in 64 registers per lane: the
+# SLP vectorizer's packed f32 pairs cost it ~20 registers of shuffles and
+# pushed it into scratch
+$(OBJ)/fbank.o: HIPFLAGS += -fno-slp-vectorize
+
 # the fast fbank mode is not bit-exact by design: let it contract mul/add
 $(OBJ)/fbank_fast.o: HIPFLAGS += -ffp-contract=fast
 

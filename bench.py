@@ -50,7 +50,7 @@ HBM_PEAK_GBS = 8000.0
 METRIC = "acoustic frames/sec (fbank->nnet posteriors), 16kHz, 1/2/4/8 GPU"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)  # 0.15 s of GPU time at C3: steady state
@@ -92,6 +92,10 @@ def parse():
     ap.add_argument("--c3-dump", default=None,
                     help="c3, tests only: write every step's log-likelihood rows (every rank its own, as "
                          "sent; rank 0 also every peer's, as received) to this .npz (.rankR.npz at N > 1)")
+    ap.add_argument("--verify-serial", action="store_true",
+                    help="c3, tests only: keep every batch's fbank / CMVN output and per-row log-likelihood sums as "
+                         "the pipelined streams produced them, then re-score every batch serially on one stream "
+                         "in the same process and report each difference (the line gains a 'verify' object)")
     ap.add_argument("--as-rank", type=int, default=None,
                     help="c3, tests only: use this rank's PCM pool (one process reproducing one rank)")
     ap.add_argument("--fbank", choices=["exact", "fast"], default="exact",
@@ -108,7 +112,7 @@ def parse():
     ap.add_argument("--back-streams", type=int, default=3,
                     help="nnet streams; consecutive batches alternate between them so one batch's "
                          "wave-quantisation tail overlaps the next batch's layers")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def usable_cores():
@@ -635,8 +639,42 @@ def _c4_keep(dump, utts, frames, rows):
     assert at == rows.shape[0]
 
 
-def main():
-    args = parse()
+def verify_serial(args, kept, ctx, model, plan, pcm, gstats, U, pool):
+    """Re-score every batch the pipelined run scored, one at a time on one
+    stream, and compare bit for bit with what the pipeline produced: the
+    fbank output, the CMVN output and each log-likelihood row's float64 sum.
+    The reference is a deterministic CPU path (per-utterance state only,
+    src/ce_stt.cc:53-60), so scheduling may not change a bit."""
+    import torch
+
+    from catears_amd import gpu
+    torch.cuda.synchronize()
+    raw = torch.empty_like(kept[0][0])
+    norm = torch.empty_like(raw) if gstats is not None else raw
+    out = torch.empty((plan.total_frames, model.num_pdfs), dtype=torch.float32, device="cuda")
+    bad = []
+    for i in sorted(kept):
+        first = (i * U) % (pool - U + 1)
+        gpu.fbank(ctx, plan, pcm[first:first + U].reshape(-1), raw)
+        if gstats is not None:
+            gpu.cmvn(ctx, plan, gstats, raw, norm)
+        gpu.am_forward(ctx, model, plan, norm, out)
+        sums = out.sum(1, dtype=torch.float64)
+        praw, pnorm, psums = kept[i]
+        d_raw = (praw.view(torch.int32) != raw.view(torch.int32))
+        d_norm = (pnorm.view(torch.int32) != norm.view(torch.int32))
+        d_sum = psums.view(torch.int64) != sums.view(torch.int64)
+        if bool(d_raw.any()) or bool(d_norm.any()) or bool(d_sum.any()):
+            rows = torch.nonzero(d_raw.any(1)).flatten().tolist()
+            bad.append({"step": i, "fbank_rows": rows[:8], "fbank_rows_n": len(rows),
+                        "fbank_bands": [torch.nonzero(d_raw[r]).flatten().tolist() for r in rows[:4]],
+                        "cmvn_rows_n": int(d_norm.any(1).sum()), "loglik_rows_n": int(d_sum.sum()),
+                        "loglik_first_row": int(torch.nonzero(d_sum).flatten()[0]) if bool(d_sum.any()) else None})
+    return {"batches": len(kept), "differing": len(bad), "detail": bad[:16]}
+
+
+def main(argv=None):
+    args = parse(argv)
     if args.workload == "c2":
         return main_c2(args)
     if args.workload == "c4":
@@ -728,6 +766,7 @@ def main():
     checksum = torch.zeros((), dtype=torch.float64, device="cuda")
     fold = [torch.zeros((), dtype=torch.float64, device="cuda") for _ in backs] if args.fold_all else None
     dump = {} if args.c3_dump else None  # step -> device copy of this rank's rows
+    kept = {} if args.verify_serial else None  # step -> (fbank out, CMVN out, per-row sums) as pipelined
     # --host-io: a host caller's buffers.  PCM slots on the device are
     # refilled from pinned host memory on an upload stream; each batch's
     # log-likelihoods go back to a pinned host ring on a download stream,
@@ -775,15 +814,20 @@ def main():
             stream.wait_event(hio["down_done"][o])  # ... and its log-likelihoods are on the host
         stream.wait_event(ready[slot])
         gpu.am_forward(ctxs[b], model, plan, norm[slot], outs[o])
-        free[slot].record(stream)
-        if fold is not None:
+        if fold is not None or kept is not None:
+            # (before free[slot] is recorded: the front stream may refill
+            # this slot as soon as it is)
             with torch.cuda.stream(stream):
-                fold[b] += outs[o].double().sum()
+                if fold is not None:
+                    fold[b] += outs[o].double().sum()
                 if dump is not None:
                     dump[i] = outs[o].clone()
                     if os.environ.get("CATEARS_DUMP_FEATS"):
                         dump[f"raw{i}"] = raw[slot].clone()
                         dump[f"norm{i}"] = norm[slot].clone()
+                if kept is not None:
+                    kept[i] = (raw[slot].clone(), norm[slot].clone(), outs[o].sum(1, dtype=torch.float64))
+        free[slot].record(stream)
         ev = torch.cuda.Event()
         ev.record(stream)
         done[o] = ev
@@ -847,6 +891,11 @@ def main():
         for p, st, a in (gat.keep or []) if gat is not None else []:
             arrs[f"r{p}s{st}"] = a
         np.savez(args.c3_dump if world == 1 else args.c3_dump.replace(".npz", f".rank{rank}.npz"), **arrs)
+    verify = verify_serial(args, kept, ctx, model, plan, pcm, gstats, U, pool) if kept is not None else None
+    verify_ranks = None
+    if verify is not None and world > 1:
+        verify_ranks = [None] * world
+        dist.all_gather_object(verify_ranks, verify)
     # f16x3: no activation left the two-plane range in any batch
     overflow = any(c.overflow() for c in set(ctxs + ctx_fs))
 
@@ -1003,10 +1052,15 @@ def main():
         "int8_vs_fp32": accuracy,
         "checksum": float(checksum.item()), "finite": finite, "split_overflow": overflow,
     }
+    if verify is not None:
+        line["verify"] = verify
+        if verify_ranks is not None:
+            line["verify_ranks"] = verify_ranks
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return line
 
 
 if __name__ == "__main__":

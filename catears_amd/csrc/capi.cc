@@ -1128,6 +1128,12 @@ static int run_steps_f32(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
 // the plane kernels (tools/ab.sh).
 // Default; CATEARS_X6_F32IN=0 selects the plane-operand kernels
 // (run_steps_x6: planes written by each epilogue, bit-identical results).
+// latency mode: the last layer's slice reduce left to the finalize launch
+struct LatPending {
+  bool on = false;
+  catears::X6Gemm last;
+};
+
 static bool x6_f32in() {
   static const bool v = [] {
     const char *e = getenv("CATEARS_X6_F32IN");
@@ -1137,7 +1143,7 @@ static bool x6_f32in() {
 }
 
 static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, int ldx, int rows,
-                         const int *row_map, const float **y, int *ldy, bool defer_final) {
+                         const int *row_map, const float **y, int *ldy, LatPending *pend) {
   int max_in = 0;
   for (const Step &st : m->steps) max_in = std::max(max_in, st.gemm.kpad);
   for (const Step &st : m->steps) max_in = std::max(max_in, (st.gemm.n + 31) / 32 * 32);
@@ -1213,12 +1219,12 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
       ProfScope prof(ctx, CE_GPU_PROF_GEMM);
       if (ctx->latency) {
         // the last layer's reduce fused into the finalize launch
-        const bool defer = last && defer_final && rows <= kX6LatWindow;
+        const bool defer = last && pend != nullptr && rows <= kX6LatWindow;
         CE_TRY(launch_gemm_bf16x6_lat(ctx->stream, a, ctx->split_part.as<float>(),
                                       ctx->split_part.bytes / sizeof(float), !defer));
         if (defer) {
-          ctx->lat_pending = true;
-          ctx->lat_last = a;
+          pend->on = true;
+          pend->last = a;
         }
       } else {
         CE_TRY(launch_gemm_bf16x6(ctx->stream, a));
@@ -1455,30 +1461,30 @@ static int run_steps_i8(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, 
   return CE_GPU_OK;
 }
 
-// defer_final: the caller hands y to finalize_output only, so a latency-mode
-// last layer may leave its reduce to that launch (ctx->lat_pending)
+// pend (optional): the caller hands y to finalize_output only, so a
+// latency-mode last layer may leave its reduce to that launch -- returned in
+// *pend, never kept in the context (an error between the two calls leaves
+// nothing behind for a later call to consume)
 static int run_steps(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, int ldx, int rows,
                      const int *row_map, const uint32_t *row_edge, const float **y, int *ldy,
-                     bool defer_final = false) {
-  ctx->lat_pending = false;
+                     LatPending *pend = nullptr) {
+  if (pend) pend->on = false;
   if (m->int8) return run_steps_i8(ctx, m, x, ldx, rows, row_map, row_edge, y, ldy);
   if (m->gemm == CE_GPU_GEMM_F16X3) return run_steps_x3(ctx, m, x, ldx, rows, row_map, y, ldy);
   if (m->gemm == CE_GPU_GEMM_BF16X6_PLANES) return run_steps_x6(ctx, m, x, ldx, rows, row_map, y, ldy);
   if (m->gemm == CE_GPU_GEMM_BF16X6)
-    return x6_f32in() ? run_steps_x6f(ctx, m, x, ldx, rows, row_map, y, ldy, defer_final)
+    return x6_f32in() ? run_steps_x6f(ctx, m, x, ldx, rows, row_map, y, ldy, pend)
                       : run_steps_x6(ctx, m, x, ldx, rows, row_map, y, ldy);
   return run_steps_f32(ctx, m, x, ldx, rows, row_map, y, ldy);
 }
 
 // launch_finalize on rows first .. first + rows - 1 of run_steps' output, or
 // the fused reduce + finalize when run_steps left the last reduce pending
-static int finalize_output(ce_gpu_ctx *ctx, const float *y, int ldy, int first, int rows, int dim,
-                           bool log_softmax, const float *log_prior, const int *row_dst, float *out) {
-  if (ctx->lat_pending) {
-    ctx->lat_pending = false;
-    return launch_lat_finalize(ctx->stream, ctx->lat_last, ctx->split_part.as<float>(), first, rows, log_softmax,
+static int finalize_output(ce_gpu_ctx *ctx, const LatPending &pend, const float *y, int ldy, int first, int rows,
+                           int dim, bool log_softmax, const float *log_prior, const int *row_dst, float *out) {
+  if (pend.on)
+    return launch_lat_finalize(ctx->stream, pend.last, ctx->split_part.as<float>(), first, rows, log_softmax,
                                log_prior, row_dst, out);
-  }
   return launch_finalize(ctx->stream, y + (size_t)first * ldy, ldy, rows, dim, log_softmax, log_prior, row_dst,
                          out);
 }
@@ -1559,9 +1565,10 @@ int ce_gpu_am_forward(ce_gpu_ctx *ctx, const ce_gpu_model *m, const ce_gpu_plan 
     const float *y = nullptr;
     int ldy = 0;
     const uint32_t *row_edge = p->d_row_edge.as<uint32_t>() + c.map_base;
-    CE_TRY(run_steps(ctx, m, d_feats, m->input_dim, c.rows, row_src, row_edge, &y, &ldy, true));
+    LatPending pend;
+    CE_TRY(run_steps(ctx, m, d_feats, m->input_dim, c.rows, row_src, row_edge, &y, &ldy, &pend));
     ProfScope prof(ctx, CE_GPU_PROF_FINALIZE);
-    CE_TRY(finalize_output(ctx, y, ldy, 0, c.rows, m->num_pdfs, m->final_log_softmax, m->log_prior.as<float>(),
+    CE_TRY(finalize_output(ctx, pend, y, ldy, 0, c.rows, m->num_pdfs, m->final_log_softmax, m->log_prior.as<float>(),
                            row_dst, d_loglik));
   }
   return CE_GPU_OK;
@@ -1608,9 +1615,10 @@ int ce_gpu_nnet_propagate(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *d
   }
   const float *y = nullptr;
   int ldy = 0;
-  CE_TRY(run_steps(ctx, m, d_in, ld_in, rows, nullptr, nullptr, &y, &ldy, true));
+  LatPending pend;
+  CE_TRY(run_steps(ctx, m, d_in, ld_in, rows, nullptr, nullptr, &y, &ldy, &pend));
   ProfScope prof(ctx, CE_GPU_PROF_FINALIZE);
-  return finalize_output(ctx, y, ldy, m->net_left, out_rows, m->num_pdfs, m->final_log_softmax,
+  return finalize_output(ctx, pend, y, ldy, m->net_left, out_rows, m->num_pdfs, m->final_log_softmax,
                          subtract_prior ? m->log_prior.as<float>() : nullptr, nullptr, d_out);
 }
 
@@ -1665,9 +1673,10 @@ int ce_gpu_nnet_propagate_blocks(ce_gpu_ctx *ctx, const ce_gpu_model *m, const f
   int ldy = 0;
   // blocks are independent: the rows a Splice reads across a block boundary
   // only feed rows that block's Narrow drops
-  CE_TRY(run_steps(ctx, m, d_in, ld_in, rows, nullptr, d_edge, &y, &ldy, true));
+  LatPending pend;
+  CE_TRY(run_steps(ctx, m, d_in, ld_in, rows, nullptr, d_edge, &y, &ldy, &pend));
   ProfScope prof(ctx, CE_GPU_PROF_FINALIZE);
-  return finalize_output(ctx, y, ldy, 0, rows, m->num_pdfs, m->final_log_softmax,
+  return finalize_output(ctx, pend, y, ldy, 0, rows, m->num_pdfs, m->final_log_softmax,
                          subtract_prior ? m->log_prior.as<float>() : nullptr, d_dst, d_out);
 }
 

@@ -65,7 +65,6 @@ constexpr int kWinLen = 400;
 constexpr int kPadded = 512;
 constexpr int kHalf = 256;   // complex FFT points
 constexpr int kMel = 40;
-constexpr int kFftGens = 7;  // split-radix generations (see tables.cc)
 
 // Tables shared by every frame; built on the host by the reference's formulas
 // and uploaded once per context.  Layout is what kernels/fbank.hip indexes.
@@ -74,11 +73,6 @@ struct FbankTables {
   float twiddle[6 * 64 * 5];        // levels 4..8, 6 x (m/4 - 2) each
   int twiddle_base[9];              // start of level lg in `twiddle`
   float kn[2 * 129];                // real-FFT post twiddles kN_k, k = 1..128
-  uint32_t fft_ops[kFftGens * 64];  // per generation, per lane node op
-  // the same ops as the lane descriptors fb::fft_lane_op executes
-  uint32_t fft_addr[kFftGens * 64];  // four swizzled LDS slots, 8 bits each
-  uint32_t fft_meta[kFftGens * 64];  // kind | twiddle case << 2
-  float fft_tw[kFftGens * 64 * 6];   // the op's six table twiddles
   int mel_off[kMel];                // first FFT bin of each triangle
   int mel_len[kMel];
   int mel_wbase[kMel];              // start of its weights in mel_w
@@ -95,6 +89,14 @@ struct FbankTables {
   int ff_slot_band[3 * 16];
   int ff_slot_start[3 * 16];
   float ff_slot_w[16 * 52];  // lane j's windows back to back at j * kFfSlotW
+  // exact kernel (fbank8_ops.h): phase-A twiddle records [op][lane r][8],
+  // the length-16 node's twiddles (n = 1, n = 3), mel slot windows: lane q
+  // of slot c starts at bin fb8_mel_st[c * 8 + q], weights at
+  // fb8_mel_w[q * kMelWTot + kMelWBase[c] ...]
+  float fb8_twa[23 * 8 * 8];
+  float fb8_tw16[12];
+  int fb8_mel_st[5 * 8];
+  float fb8_mel_w[92 * 8];
 };
 
 // fast-mode mel slot windows (bins): the 16 longest bands (<= 31 bins), the
@@ -105,12 +107,6 @@ constexpr int kFfSlotW = 52;
 
 // Builds the tables (tables.cc).
 void build_fbank_tables(FbankTables *t);
-
-// Node-op encoding for fft_ops: kind(2) | lg(4) | n(8) | base(8).
-enum FftOpKind : uint32_t { kOpNone = 0, kOpNode = 1, kOpLeaf4 = 2, kOpLeaf2 = 3 };
-inline uint32_t fft_op(uint32_t kind, uint32_t lg, uint32_t n, uint32_t base) {
-  return kind | (lg << 2) | (n << 6) | (base << 14);
-}
 
 // -------------------------------------------------------------- nnet ops --
 
@@ -306,10 +302,6 @@ struct ce_gpu_ctx {
   int latency = 0;             // ce_gpu_ctx_set_latency: split-K GEMMs for small batches
   int fbank_mode = 0;          // ce_gpu_ctx_set_fbank: CE_GPU_FBANK_EXACT / _FAST
   catears::DevBuf split_part;  // latency mode: GEMM slice partials (grown on demand)
-  // latency mode: the last layer's slice reduce left to the finalize launch
-  // (run_steps with defer_final; consumed by finalize_output in capi.cc)
-  bool lat_pending = false;
-  catears::X6Gemm lat_last;
   std::vector<int32_t> h_blk_maps;
   // optional per-class launch timing (ce_gpu_ctx_profile)
   bool profiling = false;

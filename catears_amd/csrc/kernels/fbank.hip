@@ -1,41 +1,46 @@
-// fbank.hip -- batched log-mel filterbank on gfx950.
+// fbank.hip -- batched log-mel filterbank on gfx950, the reference's
+// operation order (exact mode, the default).
 //
 // Replaces the per-frame loop of Fbank::Process (src/fbank.cc:297-303):
 // ExtractWindow + ProcessWindow (fbank.cc:44-100), SRFFT::Compute
 // (srfft.cc:370-459), ComputePowerSpectrum (fbank.cc:193-211),
 // Melbanks::Compute (fbank.cc:165-184), floor + log (fbank.cc:243-244).
 //
-// Mapping: one wave (64 lanes) per frame, four frames per 256-thread block,
-// frames of every utterance of the batch flattened into one grid.
-//   1. the frame's 400 samples are read once from HBM (7 coalesced loads per
-//      lane), the DC mean is a wave reduction;
-//   2. pre-emphasis (double, as the reference) and the Hamming window are
-//      applied while scattering even/odd samples into the wave's complex
-//      re/im arrays in LDS (the real->complex packing of srfft.cc:318-324);
-//   3. the 256-point split-radix complex FFT runs as 7 generations of lane
-//      ops (tables.cc), each lane op touching 4 points in registers;
-//   4. real-FFT post-pass + power spectrum for two k per lane, reading the
-//      FFT output at bit-reversed positions instead of permuting it;
-//   5. lanes 0..39 each form one mel energy (sequential dot, as the
-//      reference), floor at FLT_EPSILON, logf, and store one row of 40 floats.
-// Everything up to the final logf is the reference's float arithmetic in the
-// reference's order (the DC sum is exact for integer-valued PCM, whose partial
-// sums are integers below 2^24), so pre-log mel energies match bit for bit.
+// Mapping (fbank8_ops.h): eight lanes per frame, eight frames per wave.
+//   1. lane r reads the frame's samples 16j + 2r, +1 (and the sample before
+//      each pair); the DC sum is an exact butterfly over the frame's lanes;
+//   2. DC removal, pre-emphasis (double, as the reference) and the Hamming
+//      window give the lane's complex points r + 8j in registers;
+//   3. phase A: the 23 node ops of the length-256/128/64/32 nodes that touch
+//      the lane's residue class mod 8, in registers;
+//   4. one transpose through the wave's LDS (re, then im), then phase B: the
+//      length-16/8/4/2 nodes of the lane's two 16-point blocks, in registers;
+//   5. the FFT output back to LDS; the real-FFT post-pass + power spectrum
+//      for 16 k per lane (bit-reversed reads), power into LDS;
+//   6. five mel bands per lane over zero-padded 4-aligned windows (16-byte
+//      LDS reads), floor at FLT_EPSILON, logf, store.
+// Every float operation up to the final logf is the reference's, in the
+// reference's order, so pre-log mel energies match bit for bit (the CPU
+// emulator of the same lane program, tests/native/emu_fbank.cc, and the GPU
+// parity tests check it).  The kernel keeps every value in registers or LDS
+// (no scratch: tests/test_abi.py).
 #include <float.h>
 #include <hip/hip_runtime.h>
 
-#include "../fbank_ops.h"
+#include "../fbank8_ops.h"
 #include "../internal.h"
 
 namespace catears {
 namespace {
 
-constexpr int kFramesPerBlock = 4;  // one wave per frame, 4 waves per block
-#ifndef FBANK_GENS
-#define FBANK_GENS kFftGens  // (timing experiments only may lower it)
+using namespace fb8;
+
+constexpr int kFramesPerBlock = 4;  // granularity of the plan's block_utt table
+#ifndef FBANK_WAVES
+#define FBANK_WAVES 8
 #endif
-constexpr int kBlocksPerCU = 5;     // residency of fbank_kernel (27 KB LDS, 96 VGPRs)
-constexpr int kMaxBlocks = 256 * kBlocksPerCU;
+constexpr int kWaves = FBANK_WAVES;  // waves per block (8 frames each)
+constexpr int kBlocksPerCU = 2;      // LDS: 8 x 8 x 1056 B of frame regions + 11.5 KB of tables
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -43,143 +48,124 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-  return v;
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
 }
 
-struct WaveSmem {
-  float x[kWinLen];   // mean-removed samples, later the power spectrum
-  float re[kHalf];
-  float im[kHalf];
+// frame-independent tables, staged once per (persistent) block
+struct Fb8Lds {
+  float twa[kOpsA * kLanes * kTwA];
+  float win[kWinLen];
+  float kn[2 * 129];
+  float melw[kMelWTot * kLanes];
+  int mel_st[kMelSlots * kLanes];
 };
 
-// Tables staged once per block in LDS (indexed by generation / band at run
-// time): each lane op's twiddles and the mel weights (the op's slots and
-// kind live in the lane's registers).
-struct BlockTables {
-  float tw[kFftGens * 64 * 6];  // each lane op's six twiddles
-  float mel_w[512];
-};
-
-// Persistent blocks: each block stages the frame-independent tables once --
-// into LDS what is indexed at run time (twiddles, generation ops, mel
-// weights), into registers what depends only on the lane (window taps,
-// post-pass twiddles and LDS slots, the lane's mel band) -- then its four
-// waves walk frames f = 4 * block + wave, f += 4 * gridDim.x.  Per frame the
-// only global traffic is the 1.6 kB PCM read and the 160 B feature write.
-// 5 waves per SIMD (the LDS bound; unrolled, the compiler would otherwise
-// take 117 VGPRs and 4 waves)
-// Sample: float (raw int16 scale, the Vector<float> WaveReader::Process
-// produces) or int16_t (the WAV payload itself, converted here exactly as
-// src/pcm_reader.cc:174 does on the host -- int16 -> float is exact, so both
-// inputs give the same bits; 2 B per sample read instead of 4).
-template <typename Sample>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) void fbank_kernel(const FbankTables *__restrict__ tab,
-                                                    const Sample *__restrict__ pcm,
-                                                    const int64_t *__restrict__ sample_off,
-                                                    const int64_t *__restrict__ frame_off,
-                                                    const int *__restrict__ block_utt,
-                                                    int64_t total_frames, float *__restrict__ feats,
-                                                    float *__restrict__ mel_out) {
-  __shared__ WaveSmem smem[kFramesPerBlock];
-  __shared__ BlockTables bt;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int i = threadIdx.x; i < kFftGens * 64 * 6; i += 256) bt.tw[i] = tab->fft_tw[i];
-  for (int i = threadIdx.x; i < 512; i += 256) bt.mel_w[i] = tab->mel_w[i];
-  float win[7];
+// MEL: also store the pre-log mel energies (a template argument: a branch on
+// the pointer inside the frame loop cost ~57 registers)
+template <typename Sample, bool MEL>
+__global__ __launch_bounds__(kWaves * 64, 4) void fbank_kernel(const FbankTables *__restrict__ tab,
+                                                            const Sample *__restrict__ pcm,
+                                                            const int64_t *__restrict__ sample_off,
+                                                            const int64_t *__restrict__ frame_off,
+                                                            const int *__restrict__ block_utt, int64_t total_frames,
+                                                            float *__restrict__ feats, float *__restrict__ mel_out) {
+  __shared__ __attribute__((aligned(16))) float lds[kWaves * kLanes * kStride];
+  __shared__ __attribute__((aligned(16))) Fb8Lds T;
+  for (int i = threadIdx.x; i < kOpsA * kLanes * kTwA; i += kWaves * 64) T.twa[i] = tab->fb8_twa[i];
+  for (int i = threadIdx.x; i < kWinLen; i += kWaves * 64) T.win[i] = tab->window[i];
+  for (int i = threadIdx.x; i < 2 * 129; i += kWaves * 64) T.kn[i] = tab->kn[i];
+  for (int i = threadIdx.x; i < kMelWTot * kLanes; i += kWaves * 64) T.melw[i] = tab->fb8_mel_w[i];
+  for (int i = threadIdx.x; i < kMelSlots * kLanes; i += kWaves * 64) T.mel_st[i] = tab->fb8_mel_st[i];
+  const int lane0 = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float tw16[12];
 #pragma unroll
-  for (int j = 0; j < 7; ++j) {
-    const int i = lane + 64 * j;
-    win[j] = i < kWinLen ? tab->window[i] : 0.0f;
-  }
-  const int k0 = lane + 1, k1 = lane + 65;
-  const float kn0r = tab->kn[2 * k0], kn0i = tab->kn[2 * k0 + 1];
-  const float kn1r = tab->kn[2 * k1], kn1i = tab->kn[2 * k1 + 1];
-  const int a0 = fb::sw(fb::bitrev8(k0)), b0 = fb::sw(fb::bitrev8(256 - k0));
-  const int a1 = fb::sw(fb::bitrev8(k1)), b1 = fb::sw(fb::bitrev8((256 - k1) & 255));
-  // this lane's FFT op slots and kinds for every generation, in registers
-  // (the frame loop then needs no descriptor load before its LDS accesses)
-  uint32_t gaddr[kFftGens];
-  uint32_t gmeta = 0;
-#pragma unroll
-  for (int g = 0; g < kFftGens; ++g) {
-    gaddr[g] = tab->fft_addr[g * 64 + lane];
-    gmeta |= (tab->fft_meta[g * 64 + lane] & 15u) << (4 * g);
-  }
-  const int band = lane < kMel ? lane : 0;
-  const int mel_off = tab->mel_off[band], mel_len = lane < kMel ? tab->mel_len[band] : 0;
-  const int mel_wbase = tab->mel_wbase[band];
+  for (int i = 0; i < 12; ++i) tw16[i] = tab->fb8_tw16[i];  // uniform: scalar loads
   __syncthreads();
 
-  WaveSmem &S = smem[wave];
-  const int64_t stride = (int64_t)gridDim.x * kFramesPerBlock;
-  for (int64_t f = (int64_t)blockIdx.x * kFramesPerBlock + wave; f < total_frames; f += stride) {
-    int u = block_utt[f / kFramesPerBlock];
-    while (f >= frame_off[u + 1]) ++u;
-    const Sample *src = pcm + sample_off[u] + (f - frame_off[u]) * kShift;
+  const int64_t stride = (int64_t)gridDim.x * kWaves;
+  for (int64_t g = (int64_t)blockIdx.x * kWaves + wave; g * kLanes < total_frames; g += stride) {
+    // the lane index, opaque per group of frames: the lane's LDS / table
+    // addresses are re-derived here (a few adds) instead of being hoisted out
+    // of the loop, where dozens of them would stay live in registers
+    int lane = lane0;
+    asm volatile("" : "+v"(lane));
+    const int r = lane & 7, fs = lane >> 3;
+    float *fbuf = lds + (wave * kLanes + fs) * kStride;
+    const int64_t f = g * kLanes + fs;
+    const int64_t fc = f < total_frames ? f : total_frames - 1;
+    int u = block_utt[fc / kFramesPerBlock];
+    while (fc >= frame_off[u + 1]) ++u;
+    const Sample *src = pcm + sample_off[u] + (fc - frame_off[u]) * kShift;
 
-    // 1. samples + DC offset (sum exact for integer-valued PCM: any order)
-    float v[7];
-    float part = 0.0f;
-#pragma unroll
-    for (int j = 0; j < 7; ++j) {
-      const int i = lane + 64 * j;
-      v[j] = i < kWinLen ? (float)src[i] : 0.0f;
-      part += v[j];
+    // 1-2. samples, DC offset, pre-emphasis, window
+    float re[kPts], im[kPts];
+    {
+      float part = lane_sum(src, r);
+      // the frame's eight lanes: quad butterflies, then the other quad of
+      // the eight (row_half_mirror); exact integer sums, any order
+      part += dpp_f<0xB1>(part);   // quad_perm [1,0,3,2]
+      part += dpp_f<0x4E>(part);   // quad_perm [2,3,0,1]
+      part += dpp_f<0x141>(part);  // row_half_mirror
+      // (the compiler may not reuse the first pass's loads here: that
+      // would keep all 75 samples live at once)
+      asm volatile("" ::: "memory");
+      lane_window(src, part / (float)kWinLen, r, T.win, re, im);
     }
-    const float mean = wave_sum(part) / (float)kWinLen;
-#pragma unroll
-    for (int j = 0; j < 7; ++j) {
-      const int i = lane + 64 * j;
-      if (i < kWinLen) S.x[i] = v[j] - mean;
+    // 3. phase A in registers
+    phase_a(re, im, r, [&](int t) { return T.twa + (t * kLanes + r) * kTwA; });
+    // 4. transpose, phase B in registers
+    store_a(re, r, fbuf);
+    wave_sync();
+    load_b(r, fbuf, re);
+    wave_sync();
+    store_a(im, r, fbuf);
+    wave_sync();
+    load_b(r, fbuf, im);
+    phase_b(re, im, r, tw16);
+    wave_sync();
+    // 5. real-FFT post-pass + power spectrum
+    float xr[16], yr[16], xi[16], yi[16];
+    __builtin_amdgcn_sched_barrier(0);
+    store_b(r, re, fbuf);
+    wave_sync();
+    load_post(r, fbuf, xr, yr);
+    const float e0r = fbuf[0];
+    wave_sync();
+    store_b(r, im, fbuf);
+    wave_sync();
+    load_post(r, fbuf, xi, yi);
+    const float e0i = fbuf[0];
+    wave_sync();
+    __builtin_amdgcn_sched_barrier(0);
+    post_store(r, xr, xi, yr, yi, T.kn, fbuf);
+    if (r == 0) {  // DC and Nyquist bins (srfft.cc:446-451, fbank.cc:203-204)
+      const float z = e0r + e0i, nyq = e0r - e0i;
+      fbuf[0] = z * z;
+      fbuf[256] = nyq * nyq;
     }
     wave_sync();
-
-    // 2. pre-emphasis, window, pack even/odd samples as re/im, zero pad
+    // 6. mel energies, floor, log
+    int st[kMelSlots];
 #pragma unroll
-    for (int j = 0; j < 7; ++j) {
-      const int i = lane + 64 * j;
-      if (i < kWinLen) {
-        const float cur = S.x[i];
-        const float prev = i > 0 ? S.x[i - 1] : cur;
-        const float y = fb::preemph(cur, prev) * win[j];
-        if (i & 1)
-          S.im[fb::sw(i >> 1)] = y;
-        else
-          S.re[fb::sw(i >> 1)] = y;
-      }
-    }
-    if (lane < kHalf - kWinLen / 2) {
-      S.re[fb::sw(kWinLen / 2 + lane)] = 0.0f;
-      S.im[fb::sw(kWinLen / 2 + lane)] = 0.0f;
-    }
-    wave_sync();
-
-    // 3. split-radix generations, unrolled: each generation reads its own
-    // descriptor register (a rolled loop rotated the seven descriptors
-    // through the registers, 7 moves per generation: 2 % slower)
+    for (int c = 0; c < kMelSlots; ++c) st[c] = T.mel_st[c * kLanes + r];
+    float e[kMelSlots];
+    e[0] = mel_window<8>(T.melw + r * kMelWTot + kMelWBase[0], fbuf + st[0]);
+    e[1] = mel_window<12>(T.melw + r * kMelWTot + kMelWBase[1], fbuf + st[1]);
+    e[2] = mel_window<16>(T.melw + r * kMelWTot + kMelWBase[2], fbuf + st[2]);
+    e[3] = mel_window<24>(T.melw + r * kMelWTot + kMelWBase[3], fbuf + st[3]);
+    e[4] = mel_window<32>(T.melw + r * kMelWTot + kMelWBase[4], fbuf + st[4]);
+    wave_sync();  // the frame region is rewritten by the next group of frames
+    // lanes past the last frame computed that frame (fc) bit for bit, so
+    // they store the same values to the same row: no divergent branch (one
+    // costs ~70 registers here, the compiler's choice)
 #pragma unroll
-    for (int g = 0; g < FBANK_GENS; ++g) {
-      const int o = g * 64 + lane;
-      fb::fft_lane_op(gaddr[g], (gmeta >> (4 * g)) & 15u, bt.tw + 6 * o, S.re, S.im);
-      wave_sync();
+    for (int c = 0; c < kMelSlots; ++c) {
+      const int b = 8 * c + r;
+      if (MEL) mel_out[fc * kMel + b] = e[c];
+      feats[fc * kMel + b] = logf(e[c] < FLT_EPSILON ? FLT_EPSILON : e[c]);
     }
-
-    // 4. real-FFT post-pass + power spectrum into S.x[0..256]
-    fb::post_power_ab(k0, a0, b0, S.re, S.im, kn0r, kn0i, S.x);
-    fb::post_power_ab(k1, a1, b1, S.re, S.im, kn1r, kn1i, S.x);
-    if (lane == 0) fb::edge_power(S.re, S.im, S.x);
-    wave_sync();
-
-    // 5. mel energies, floor, log
-    if (lane < kMel) {
-      const float e = fb::mel_dot(bt.mel_w + mel_wbase, S.x + mel_off, mel_len);
-      if (mel_out) mel_out[f * kMel + lane] = e;
-      feats[f * kMel + lane] = logf(e < FLT_EPSILON ? FLT_EPSILON : e);
-    }
-    wave_sync();  // S.x is rewritten by the next frame
   }
 }
 
@@ -187,9 +173,15 @@ template <typename Sample>
 int launch_fbank_t(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, const Sample *pcm, float *feats,
                    float *mel) {
   if (p->total_frames == 0) return CE_GPU_OK;
-  const int64_t blocks = (p->total_frames + kFramesPerBlock - 1) / kFramesPerBlock;
-  const unsigned grid = (unsigned)(blocks < kMaxBlocks ? blocks : kMaxBlocks);
-  hipLaunchKernelGGL(fbank_kernel<Sample>, dim3(grid), dim3(256), 0, s, d_tab, pcm,
+  const int64_t per_block = kWaves * kLanes, blocks = (p->total_frames + per_block - 1) / per_block;
+  const int64_t max_blocks = 256 * kBlocksPerCU;
+  const unsigned grid = (unsigned)(blocks < max_blocks ? blocks : max_blocks);
+  if (mel)
+    hipLaunchKernelGGL((fbank_kernel<Sample, true>), dim3(grid), dim3(kWaves * 64), 0, s, d_tab, pcm,
+                     p->d_sample_off.as<int64_t>(), p->d_frame_off.as<int64_t>(),
+                     p->d_block_utt.as<int>(), p->total_frames, feats, mel);
+    else
+    hipLaunchKernelGGL((fbank_kernel<Sample, false>), dim3(grid), dim3(kWaves * 64), 0, s, d_tab, pcm,
                      p->d_sample_off.as<int64_t>(), p->d_frame_off.as<int64_t>(),
                      p->d_block_utt.as<int>(), p->total_frames, feats, mel);
   CE_HIP(hipGetLastError());

@@ -121,7 +121,10 @@ __global__ __launch_bounds__(64 * kLatNW, MULTI && TF == 4 && KT <= 6 ? 2 : 1) v
       const int seg = k / p.din, segc = min(seg, p.nseg - 1);
       const int shift = (int)(signed char)(p.off_packed >> (8 * segc));
       xrow[j] = clampi(clampi(f0 + prow, 0, p.m - 1) + shift, 0, p.m - 1);
-      xcol[j] = k - segc * p.din;
+      // K's zero padding past the last segment: the value is masked out
+      // (xlive), but the address must stay inside the row -- column 0 -- or
+      // the last source row's load could run past the end of the buffer
+      xcol[j] = seg < p.nseg ? k - segc * p.din : 0;
       xlive[j] = tid + j * NT < TASKS && i < nk && seg < p.nseg && !(DIAG & 2);
     }
     if (p.row_map) {

@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <vector>
 
+#include "fbank8_ops.h"
 #include "fbank_ops.h"
 #include "internal.h"
 
@@ -104,83 +105,6 @@ void build_post_twiddles(FbankTables *t) {
   }
 }
 
-// The split-radix recursion (srfft.cc:124-265) as a DAG of node ops.  A node
-// of length m = 2^lg (lg >= 3) becomes m/4 lane ops: lane n owns points n,
-// n+m/4, n+m/2, n+3m/4 and performs the node's step-1 butterflies, step-2
-// rotation and step-3/4 twiddles on them, in the reference's operation order.
-// Nodes of length 4 and 2 are one lane op each.  Independent ops are packed
-// into generations of <= 64 lanes (one wave); a node's children go to a later
-// generation than the node itself.
-struct Pending {
-  int lg, base, ready;
-};
-
-void build_fft_schedule(FbankTables *t) {
-  std::vector<std::vector<uint32_t>> gens(4 * kFftGens);
-  std::vector<Pending> pending = {{8, 0, 0}};
-  while (!pending.empty()) {
-    // earliest-ready first; among equals the longest node (deepest subtree),
-    // so leaves, which have no successors, absorb any generation overflow
-    size_t pick = 0;
-    for (size_t i = 1; i < pending.size(); ++i) {
-      const Pending &a = pending[i], &b = pending[pick];
-      if (a.ready < b.ready || (a.ready == b.ready && a.lg > b.lg)) pick = i;
-    }
-    Pending p = pending[pick];
-    pending.erase(pending.begin() + pick);
-    if (p.lg == 0) continue;
-    const int width = p.lg >= 3 ? (1 << p.lg) / 4 : 1;
-    int g = p.ready;
-    while ((int)gens[g].size() + width > 64) ++g;  // list scheduling
-    if (p.lg >= 3) {
-      for (int n = 0; n < width; ++n) gens[g].push_back(fft_op(kOpNode, p.lg, n, p.base));
-      const int m = 1 << p.lg;
-      pending.push_back({p.lg - 1, p.base, g + 1});
-      pending.push_back({p.lg - 2, p.base + m / 2, g + 1});
-      pending.push_back({p.lg - 2, p.base + 3 * (m / 4), g + 1});
-    } else {
-      gens[g].push_back(fft_op(p.lg == 2 ? kOpLeaf4 : kOpLeaf2, p.lg, 0, p.base));
-    }
-  }
-  for (size_t g = kFftGens; g < gens.size(); ++g)
-    if (!gens[g].empty()) abort();  // schedule must fit kFftGens generations
-  for (int g = 0; g < kFftGens; ++g)
-    for (int l = 0; l < 64; ++l)
-      t->fft_ops[g * 64 + l] = l < (int)gens[g].size() ? gens[g][l] : fft_op(kOpNone, 0, 0, 0);
-}
-
-// Lane descriptors of the scheduled ops (fbank_ops.h fft_lane_op): the LDS
-// slots and twiddle values each op touches, resolved on the host so the
-// kernel's lanes do no index arithmetic.
-void build_fft_lanes(FbankTables *t) {
-  for (int i = 0; i < kFftGens * 64; ++i) {
-    const uint32_t op = t->fft_ops[i];
-    const uint32_t kind = op & 3u;
-    const int lg = (int)((op >> 2) & 15u), n = (int)((op >> 6) & 255u), base = (int)(op >> 14);
-    int pts[4] = {0, 0, 0, 0};
-    uint32_t twc = 0;
-    if (kind == kOpLeaf2) {
-      pts[0] = base, pts[1] = base + 1, pts[2] = base, pts[3] = base + 1;
-    } else if (kind == kOpLeaf4) {
-      for (int j = 0; j < 4; ++j) pts[j] = base + j;
-    } else if (kind == kOpNode) {
-      const int q = 1 << (lg - 2), h = 2 * q, e = q / 2;
-      pts[0] = base + n, pts[1] = base + n + q, pts[2] = base + n + h, pts[3] = base + n + h + q;
-      if (n == e) {
-        twc = 1;
-      } else if (n > 0) {
-        twc = 2;
-        const int nel = q - 2, w = n - 1 - (n > e ? 1 : 0);
-        for (int j = 0; j < 6; ++j) t->fft_tw[i * 6 + j] = t->twiddle[t->twiddle_base[lg] + j * nel + w];
-      }
-    }
-    uint32_t addr = 0;
-    for (int j = 0; j < 4; ++j) addr |= (uint32_t)fb::sw(pts[j]) << (8 * j);
-    t->fft_addr[i] = addr;
-    t->fft_meta[i] = kind | (twc << 2);
-  }
-}
-
 // Fast-mode tables: the four-step FFT's inter-pass twiddles, the real-FFT
 // post twiddles (both in double, rounded once) and the 40 mel bands in three
 // fixed-size slots of a frame's 16 lanes (zero-padded weight windows).
@@ -216,6 +140,34 @@ void build_fast(FbankTables *t) {
   }
 }
 
+// Exact-kernel tables (fbank8_ops.h): each lane's phase-A twiddle records,
+// the length-16 node's, and the mel slot windows.
+void build_fb8(FbankTables *t) {
+  auto twid = [&](int lg, int n, float *dst) {
+    const int q = 1 << (lg - 2), e = q / 2, nel = q - 2;
+    if (n == 0 || n == e) return;  // no table twiddles (srfft.cc:230-239)
+    const int w = n - 1 - (n > e ? 1 : 0);
+    for (int j = 0; j < 6; ++j) dst[j] = t->twiddle[t->twiddle_base[lg] + j * nel + w];
+  };
+  for (int op = 0; op < fb8::kOpsA; ++op)
+    for (int r = 0; r < fb8::kLanes; ++r) {
+      int lg, n;
+      fb8::phase_a_op(op, r, &lg, &n);
+      twid(lg, n, t->fb8_twa + (op * fb8::kLanes + r) * fb8::kTwA);
+    }
+  twid(4, 1, t->fb8_tw16);
+  twid(4, 3, t->fb8_tw16 + 6);
+  for (int c = 0; c < fb8::kMelSlots; ++c)
+    for (int q = 0; q < fb8::kLanes; ++q) {
+      const int b = 8 * c + q, W = fb8::kMelW[c];
+      const int st = std::min(t->mel_off[b] & ~3, kHalf - W);
+      if (t->mel_off[b] < st || t->mel_off[b] + t->mel_len[b] > st + W) abort();  // fixed geometry (src/fbank.h)
+      t->fb8_mel_st[c * fb8::kLanes + q] = st;
+      float *w = t->fb8_mel_w + q * fb8::kMelWTot + fb8::kMelWBase[c];
+      for (int i = 0; i < t->mel_len[b]; ++i) w[t->mel_off[b] - st + i] = t->mel_w[t->mel_wbase[b] + i];
+    }
+}
+
 }  // namespace
 
 void build_fbank_tables(FbankTables *t) {
@@ -224,9 +176,8 @@ void build_fbank_tables(FbankTables *t) {
   build_mel(t);
   build_twiddles(t);
   build_post_twiddles(t);
-  build_fft_schedule(t);
-  build_fft_lanes(t);
   build_fast(t);
+  build_fb8(t);
 }
 
 }  // namespace catears

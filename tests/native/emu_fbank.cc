@@ -1,18 +1,21 @@
-// emu_fbank.cc -- TEST HARNESS.  Runs the fbank kernel's lane schedule on the
-// CPU: the same table builder (csrc/tables.cc) and the same per-lane
-// arithmetic (csrc/fbank_ops.h) as kernels/fbank.hip, executing each wave
-// generation's 64 lane ops one after another (they are independent by
-// construction).  tests/test_emulation.py compares its pre-log mel energies
+// emu_fbank.cc -- TEST HARNESS.  Runs the exact fbank kernel's lane program
+// on the CPU: the same table builder (csrc/tables.cc) and the same per-lane
+// code (csrc/fbank8_ops.h) as kernels/fbank.hip, the eight lanes of a frame
+// one after another between the kernel's synchronisation points, with a
+// frame-sized array standing in for the wave's LDS region (each lane writes
+// only its own points before a sync and reads any after it, so this order is
+// the kernel's).  tests/test_emulation.py compares the pre-log mel energies
 // bit for bit with the oracle, which proves the decomposition on a CPU.
 // Never linked into the product.
 #include <float.h>
 #include <math.h>
 #include <string.h>
 
-#include "fbank_ops.h"
+#include "fbank8_ops.h"
 #include "internal.h"
 
 using namespace catears;
+using namespace catears::fb8;
 
 extern "C" int emu_fbank(const float *wave, long n, float *mel, float *feats) {
   static FbankTables tab;
@@ -24,43 +27,55 @@ extern "C" int emu_fbank(const float *wave, long n, float *mel, float *feats) {
   const int frames = n < kWinLen ? 0 : (int)(1 + (n - kWinLen) / kShift);
   for (int f = 0; f < frames; ++f) {
     const float *src = wave + (long)f * kShift;
-    float x[kWinLen], re[kHalf], im[kHalf], pw[kHalf + 1];
-    // wave-reduction order of the kernel: per-lane partial over j, then
-    // butterfly over lanes (xor 32, 16, ..., 1)
-    float part[64];
-    for (int l = 0; l < 64; ++l) {
-      part[l] = 0.0f;
-      for (int j = 0; j < 7; ++j) {
-        int i = l + 64 * j;
-        part[l] += i < kWinLen ? src[i] : 0.0f;
-      }
-    }
-    for (int d = 32; d >= 1; d >>= 1) {
-      float nxt[64];
-      for (int l = 0; l < 64; ++l) nxt[l] = part[l] + part[l ^ d];
+    float re[kLanes][kPts], im[kLanes][kPts];
+    float part[kLanes];
+    float lds[kStride];
+    for (int r = 0; r < kLanes; ++r) part[r] = lane_sum(src, r);
+    // the kernel's butterfly over the frame's eight lanes (xor 1, 2, 4)
+    for (int d = 1; d < kLanes; d <<= 1) {
+      float nxt[kLanes];
+      for (int r = 0; r < kLanes; ++r) nxt[r] = part[r] + part[r ^ d];
       memcpy(part, nxt, sizeof(part));
     }
-    const float mean = part[0] / (float)kWinLen;
-    for (int i = 0; i < kWinLen; ++i) x[i] = src[i] - mean;
-    for (int i = 0; i < kWinLen; ++i) {
-      float y = fb::preemph(x[i], i > 0 ? x[i - 1] : x[i]) * tab.window[i];
-      if (i & 1) im[fb::sw(i >> 1)] = y; else re[fb::sw(i >> 1)] = y;
+    for (int r = 0; r < kLanes; ++r) {
+      lane_window(src, part[r] / (float)kWinLen, r, tab.window, re[r], im[r]);
+      phase_a(re[r], im[r], r, [&](int t) { return tab.fb8_twa + (t * kLanes + r) * kTwA; });
     }
-    for (int i = kWinLen / 2; i < kHalf; ++i) re[fb::sw(i)] = im[fb::sw(i)] = 0.0f;
-    for (int g = 0; g < kFftGens; ++g)
-      for (int l = 0; l < 64; ++l) {
-        const int o = g * 64 + l;
-        fb::fft_lane_op(tab.fft_addr[o], tab.fft_meta[o], tab.fft_tw + 6 * o, re, im);
+    // transpose (re, then im) through the frame's LDS region
+    for (int r = 0; r < kLanes; ++r) store_a(re[r], r, lds);
+    for (int q = 0; q < kLanes; ++q) load_b(q, lds, re[q]);
+    for (int r = 0; r < kLanes; ++r) store_a(im[r], r, lds);
+    for (int q = 0; q < kLanes; ++q) load_b(q, lds, im[q]);
+    for (int q = 0; q < kLanes; ++q) phase_b(re[q], im[q], q, tab.fb8_tw16);
+    // FFT output back to LDS; post-pass operands
+    float xr[kLanes][16], yr[kLanes][16], xi[kLanes][16], yi[kLanes][16], e0r = 0, e0i = 0;
+    for (int q = 0; q < kLanes; ++q) store_b(q, re[q], lds);
+    for (int q = 0; q < kLanes; ++q) load_post(q, lds, xr[q], yr[q]);
+    e0r = lds[0];
+    for (int q = 0; q < kLanes; ++q) store_b(q, im[q], lds);
+    for (int q = 0; q < kLanes; ++q) load_post(q, lds, xi[q], yi[q]);
+    e0i = lds[0];
+    // power spectrum (the LDS region again), DC / Nyquist by lane 0
+    for (int q = 0; q < kLanes; ++q) post_store(q, xr[q], xi[q], yr[q], yi[q], tab.kn, lds);
+    {
+      const float z = e0r + e0i, nyq = e0r - e0i;
+      lds[0] = z * z;
+      lds[256] = nyq * nyq;
+    }
+    for (int q = 0; q < kLanes; ++q) {
+      float e[kMelSlots];
+      const float *w = tab.fb8_mel_w;
+      const int *st = tab.fb8_mel_st + q;
+      e[0] = mel_window<8>(w + q * kMelWTot + kMelWBase[0], lds + st[0 * kLanes]);
+      e[1] = mel_window<12>(w + q * kMelWTot + kMelWBase[1], lds + st[1 * kLanes]);
+      e[2] = mel_window<16>(w + q * kMelWTot + kMelWBase[2], lds + st[2 * kLanes]);
+      e[3] = mel_window<24>(w + q * kMelWTot + kMelWBase[3], lds + st[3 * kLanes]);
+      e[4] = mel_window<32>(w + q * kMelWTot + kMelWBase[4], lds + st[4 * kLanes]);
+      for (int c = 0; c < kMelSlots; ++c) {
+        const int b = 8 * c + q;
+        mel[(long)f * kMel + b] = e[c];
+        feats[(long)f * kMel + b] = logf(e[c] < FLT_EPSILON ? FLT_EPSILON : e[c]);
       }
-    for (int l = 0; l < 64; ++l) {
-      fb::post_power(l + 1, re, im, tab.kn, pw);
-      fb::post_power(l + 65, re, im, tab.kn, pw);
-    }
-    fb::edge_power(re, im, pw);
-    for (int b = 0; b < kMel; ++b) {
-      float e = fb::mel_dot(tab.mel_w + tab.mel_wbase[b], pw + tab.mel_off[b], tab.mel_len[b]);
-      mel[(long)f * kMel + b] = e;
-      feats[(long)f * kMel + b] = logf(e < FLT_EPSILON ? FLT_EPSILON : e);
     }
   }
   return frames;

@@ -4,6 +4,8 @@ import ctypes
 import os
 import re
 
+import pytest
+
 from conftest import ROOT
 
 
@@ -76,3 +78,61 @@ def test_dropin_library_defines_no_test_hook():
     hook = [ln.split() for ln in out.splitlines() if ln.endswith(" catears_test_inject_failure")]
     assert hook and all(f[-2] == "w" for f in hook), hook
     assert "InjectDeviceFailures" not in out
+
+
+def _code_objects(path):
+    """Every gfx950 code object in a HIP shared library: the .hip_fatbin
+    section holds one clang offload bundle per translation unit."""
+    import struct
+    data = open(path, "rb").read()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    objs, at = [], data.find(magic)
+    while at >= 0:
+        n = struct.unpack_from("<Q", data, at + 24)[0]
+        p = at + 32
+        for _ in range(n):
+            off, size, tlen = struct.unpack_from("<QQQ", data, p)
+            triple = data[p + 24:p + 24 + tlen].decode()
+            p += 24 + tlen
+            if "gfx950" in triple:
+                objs.append(data[at + off:at + off + size])
+        at = data.find(magic, p)
+    return objs
+
+
+def kernel_private_segments(path):
+    """{kernel symbol: .private_segment_fixed_size} from the code objects'
+    AMDGPU metadata notes (llvm-readelf --notes)."""
+    import subprocess
+    import tempfile
+    readelf = "/opt/rocm/lib/llvm/bin/llvm-readelf"
+    if not os.path.exists(readelf):
+        pytest.skip("llvm-readelf not in this image")
+    out = {}
+    for co in _code_objects(path):
+        with tempfile.NamedTemporaryFile(suffix=".co") as f:
+            f.write(co)
+            f.flush()
+            notes = subprocess.check_output([readelf, "--notes", f.name], text=True)
+        name = None
+        for ln in notes.splitlines():
+            m = re.match(r"\s+\.name:\s+(\S+)", ln)
+            if m:
+                name = m.group(1)
+            m = re.match(r"\s+\.private_segment_fixed_size:\s+(\d+)", ln)
+            if m and name:
+                out[name] = int(m.group(1))
+    return out
+
+
+def test_product_kernels_use_no_scratch():
+    """No kernel of the product library has a private (scratch) segment.
+    The exact fbank kernel once spilled 3 VGPRs to scratch under a forced
+    5-waves-per-SIMD budget and, only in the multi-stream pipeline, gave a
+    different value for one frame in some runs; every kernel
+    on the path now keeps its state in registers and LDS."""
+    segs = kernel_private_segments(os.path.join(ROOT, "catears_amd", "lib", "libcatears_hip.so"))
+    assert len(segs) >= 20, sorted(segs)
+    assert any("fbank_kernel" in k for k in segs)
+    scratch = {k: v for k, v in segs.items() if v}
+    assert not scratch, scratch

@@ -34,7 +34,7 @@ def _port():
 def _bench(extra, dump, nproc):
     env = dict(os.environ, PYTHONPATH=ROOT, CATEARS_BENCH_DEVICE="0")
     args = ["bench.py", "--workload", "c4", "--c4-utts", str(UTTS), "--model", "tdnn-xs", "--warmup", "2",
-            "--no-cpu-baseline", "--c4-dump", str(dump)] + extra
+            "--no-cpu-baseline", "--c4-dump", str(dump)] + extra  # (later --model / --c4-utts win)
     if nproc > 1:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(nproc),
                "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args + ["--dist-backend", "gloo"]
@@ -47,9 +47,23 @@ def _bench(extra, dump, nproc):
     return json.loads(line[0])
 
 
-def test_c4_two_ranks_bit_identical_to_one_process(tmp_path):
+_ONE = {}
+
+
+def _one_process(model, utts, tmp_dir):
+    """bench.py --workload c4 in one process (cached per model): the line and
+    the rows rank 0 consumed, per utterance."""
+    if model not in _ONE:
+        dump = os.path.join(str(tmp_dir), f"one_{model}.npz")
+        line = _bench(["--model", model, "--c4-utts", str(utts)], dump, 1)
+        _ONE[model] = (line, dict(np.load(dump)))
+    return _ONE[model]
+
+
+def test_c4_two_ranks_bit_identical_to_one_process(tmp_path_factory, tmp_path):
     from catears_amd.shard import c4_corpus, num_frames
-    one = _bench([], tmp_path / "one.npz", 1)
+    one, _ = _one_process("tdnn-xs", UTTS, tmp_path_factory.mktemp("c4"))
+    np.savez(tmp_path / "one.npz", **_ONE["tdnn-xs"][1])
     two = _bench([], tmp_path / "two.npz", 2)
     frames = [num_frames(int(n)) for n in c4_corpus(UTTS)]
     assert one["config"]["frames_total"] == two["config"]["frames_total"] == sum(frames)
@@ -93,8 +107,14 @@ def test_c3_two_ranks_gather_every_row(tmp_path):
     checksum folds exactly its own batches and the received ones, warm-up
     included -- no batch lost, duplicated or read before it was written."""
     steps = 6 + 2
-    two = _bench_c3(["--c3-dump", str(tmp_path / "d.npz")], 2)
+    two = _bench_c3(["--c3-dump", str(tmp_path / "d.npz"), "--verify-serial"], 2)
     assert two["n_gpus"] == 2 and two["config"]["gather"] and two["finite"]
+    # end to end: every batch each rank scored in the pipelined run (three
+    # nnet streams + the front stream + the comm stream) equals the same
+    # batch re-scored serially on one stream in the same process -- fbank,
+    # CMVN and every log-likelihood row (DESIGN.md §8b)
+    for r, v in enumerate(two["verify_ranks"]):
+        assert v["batches"] == steps and v["differing"] == 0, (r, v)
     r0, r1 = np.load(tmp_path / "d.rank0.npz"), np.load(tmp_path / "d.rank1.npz")
     assert sorted(r1.files) == sorted(f"r1s{s}" for s in range(steps))
     want = 0.0
@@ -107,3 +127,39 @@ def test_c3_two_ranks_gather_every_row(tmp_path):
     # the two ranks score different audio: a gather that dropped the peer's
     # rows (or sent rank 0's twice) would miss by a whole rank's sum
     assert not np.array_equal(r0["r0s0"], r0["r1s0"])
+
+
+@pytest.mark.parametrize("model,utts", [("tdnn-xs", UTTS), ("tdnn-s", 8)])
+def test_c4_rows_match_oracle(tmp_path_factory, model, utts):
+    """C4's gathered rows against the oracle: for the shortest and the
+    longest utterance of the length-mixed corpus, and for the utterances on
+    either side of a batch boundary (the last of one <= 4096-row batch, the
+    first of the next), rank 0's consumed rows are within the north star's
+    1e-4 of oracle.am_whole(oracle.cmvn(oracle fbank)) with an fp64 network
+    (src/am.cc:115-164 per utterance, src/ce_stt.cc:53-60: an utterance's
+    rows depend on nothing but its own samples)."""
+    import tempfile
+
+    from catears_amd import formats, synth
+    from catears_amd.shard import c4_corpus, num_frames, pack_batches, shard_utterances
+    from oracle import pyoracle
+    line, rows = _one_process(model, utts, tmp_path_factory.mktemp("c4"))
+    conf = synth.write_model(os.path.join(tempfile.gettempdir(), f"catears_bench_{os.getuid()}"), model)
+    am = formats.read_am(conf)
+    samples = c4_corpus(utts)
+    frames = [num_frames(int(n)) for n in samples]
+    mine = shard_utterances(frames, 1, 0)
+    batches = [[mine[i] for i in b] for b in pack_batches([frames[u] for u in mine], am["left"], am["right"], 4096)]
+    assert len(batches) >= 2 and line["config"]["batches_per_rank"] == [len(batches)]
+    pick = {int(np.argmin(samples)), int(np.argmax(samples)), int(batches[0][-1]), int(batches[1][0])}
+    plen = int(samples.max())
+    gstats = synth.cmvn_stats_synthetic()
+    fb = pyoracle.Fbank()
+    f64 = lambda a, w: (a.astype(np.float64) @ w.astype(np.float64)).astype(np.float32)
+    for u in sorted(pick):
+        wave = synth.pcm(600000 + u % 48, plen)[:int(samples[u])]  # bench.py main_c4's resident pool
+        ref = pyoracle.am_whole(am, pyoracle.cmvn(gstats, fb.compute(wave)), gemm=f64)
+        got = rows[f"u{u}"]
+        assert got.shape == ref.shape == (frames[u], am["log_prior"].shape[0])
+        err = float(np.abs(got - ref).max())
+        assert err <= 1e-4, (u, err)
