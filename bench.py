@@ -280,6 +280,23 @@ def init_dist(args, local):
         dist.init_process_group(args.dist_backend)
 
 
+def cpu_calibration():
+    """The port against the reference, one core each, in the build container
+    (tools/cpu_calibrate.py -> profiles/cpu_calibration.json): the port's
+    FFT time over the reference's own srfft.cc compiled there, and the port's
+    fbank / nnet rates beside the reference's (BASELINE.md:35-37)."""
+    path = os.path.join(ROOT, "profiles", "cpu_calibration.json")
+    if not os.path.exists(path):
+        return None
+    c = json.load(open(path))
+    return {"fft_port_over_reference_time": c["fft_port_over_reference_time"],
+            "port_fbank_frames_per_s_one_core": c["port_fbank_frames_per_s_one_core"],
+            "reference_fbank_frames_per_s_one_core": "190-200 k",
+            "port_nnet_frames_per_s_one_core": c["port_nnet_frames_per_s_one_core"],
+            "reference_nnet_frames_per_s_one_core": "2.5 k",
+            "source": "profiles/cpu_calibration.json (tools/cpu_calibrate.py, build container, one core)"}
+
+
 def cpu_fbank_baseline(n_utts, seconds, threads, min_wall):
     """Oracle fbank ('port') on the host cores, one utterance per worker."""
     from concurrent.futures import ThreadPoolExecutor
@@ -378,7 +395,7 @@ def main_c2(args):
         threads, how = usable_cores()
         v, fr, dt, passes = cpu_fbank_baseline(max(64, 2 * threads), args.seconds, threads, args.cpu_seconds)
         cpu = {"value": round(v, 1), "unit": "frames/s", "cores": threads, "kind": "port",
-               "per_core": round(v / threads, 1), "cores_basis": how,
+               "per_core": round(v / threads, 1), "cores_basis": how, "calibration": cpu_calibration(),
                "sample": f"{passes} passes over {max(64, 2 * threads)} x {args.seconds:g} s utterances ({fr} frames, "
                          f"{dt:.1f} s wall, {threads} worker threads): oracle fbank (C restatement of src/fbank.cc "
                          "+ srfft.cc)"}
@@ -1022,7 +1039,7 @@ def main(argv=None):
         n_cpu = max(args.cpu_utts, 2 * threads)
         v, fr, dt, passes = cpu_baseline(conf, n_cpu, args.seconds, threads, args.cpu_seconds)
         cpu = {"value": round(v, 1), "unit": "frames/s", "cores": threads, "kind": "port",
-               "per_core": round(v / threads, 1), "cores_basis": how,
+               "per_core": round(v / threads, 1), "cores_basis": how, "calibration": cpu_calibration(),
                "sample": f"{passes} passes over {n_cpu} x {args.seconds:g} s utterances ({fr} frames, "
                          f"{dt:.1f} s wall, {threads} worker threads): oracle fbank+CMVN (C) + TDNN-S with "
                          f"single-threaded OpenBLAS sgemm per worker"}

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
+#include <memory>
 #include <string>
 
 namespace catears {
@@ -86,16 +87,24 @@ static void copy2d(void *stream, hipMemcpyKind kind, void *dst, size_t dst_ld, c
 
 Runtime::Lane *Runtime::NewLane() {
   // caller holds pool_mu_ (or is the constructor)
-  Lane *l = new Lane();
+  // nothing leaks when a step throws: the lane, its stream and its context
+  // are released on the way out, and the pool is unchanged
+  std::unique_ptr<Lane> l(new Lane());
   l->index = n_lanes_;
   hip_check(hipSetDevice(device_), "hipSetDevice");
   hipStream_t s = nullptr;
   hip_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
   l->stream = s;
-  Check(ce_gpu_ctx_create(device_, l->stream, &l->ctx), "ce_gpu_ctx_create");
-  Check(ce_gpu_ctx_set_fbank(l->ctx, fbank_mode_), "ce_gpu_ctx_set_fbank");
-  lanes_[n_lanes_++] = l;
-  return l;
+  try {
+    Check(ce_gpu_ctx_create(device_, l->stream, &l->ctx), "ce_gpu_ctx_create");
+    Check(ce_gpu_ctx_set_fbank(l->ctx, fbank_mode_), "ce_gpu_ctx_set_fbank");
+  } catch (...) {
+    if (l->ctx) ce_gpu_ctx_destroy(l->ctx);
+    hipStreamDestroy(s);
+    throw;
+  }
+  lanes_[n_lanes_++] = l.get();
+  return l.release();
 }
 
 Runtime::Runtime() {

@@ -228,6 +228,12 @@ ORC_EXPORT void orc_srfft_forward(const orc_srfft *f, float *data, float *tmp) {
   data[1] = nyq;
 }
 
+/* n transforms back to back (stride = real length): timing without one
+ * foreign call per frame (tools/cpu_calibrate.py) */
+ORC_EXPORT void orc_srfft_forward_n(const orc_srfft *f, float *data, int n, float *tmp) {
+  for (int i = 0; i < n; ++i) orc_srfft_forward(f, data + (long)i * 2 * f->n_complex, tmp);
+}
+
 /* ------------------------------------------------------------------------ */
 /* Fbank, restating src/fbank.cc.                                            */
 /* ------------------------------------------------------------------------ */

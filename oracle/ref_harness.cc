@@ -22,6 +22,12 @@ void ref_srfft_forward(void *f, float *data, int real_len, float *buf) {
   static_cast<pocketkaldi::SRFFT *>(f)->Compute(data, real_len, true, buf, real_len);
 }
 
+// n forward transforms back to back (timing, tools/cpu_calibrate.py)
+void ref_srfft_forward_n(void *f, float *data, int n, int real_len, float *buf) {
+  for (int i = 0; i < n; ++i)
+    static_cast<pocketkaldi::SRFFT *>(f)->Compute(data + (long)i * real_len, real_len, true, buf, real_len);
+}
+
 // MatMat_U8U8F32 (src/matrix.cc:389-420): row-major A (m x k), B (k x n), C (m x n).
 void ref_gemm_u8u8f32(int m, int n, int k, const uint8_t *a, float sa, int32_t zpa,
                       const uint8_t *b, float sb, int32_t zpb, float *c) {
