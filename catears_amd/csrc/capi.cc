@@ -1128,12 +1128,6 @@ static int run_steps_f32(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
 // the plane kernels (tools/ab.sh).
 // Default; CATEARS_X6_F32IN=0 selects the plane-operand kernels
 // (run_steps_x6: planes written by each epilogue, bit-identical results).
-// latency mode: the last layer's slice reduce left to the finalize launch
-struct LatPending {
-  bool on = false;
-  catears::X6Gemm last;
-};
-
 static bool x6_f32in() {
   static const bool v = [] {
     const char *e = getenv("CATEARS_X6_F32IN");
@@ -1143,7 +1137,7 @@ static bool x6_f32in() {
 }
 
 static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, int ldx, int rows,
-                         const int *row_map, const float **y, int *ldy, LatPending *pend) {
+                         const int *row_map, const float **y, int *ldy) {
   int max_in = 0;
   for (const Step &st : m->steps) max_in = std::max(max_in, st.gemm.kpad);
   for (const Step &st : m->steps) max_in = std::max(max_in, (st.gemm.n + 31) / 32 * 32);
@@ -1151,21 +1145,6 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
   CE_TRY(ensure_workspace(ctx, 2 * blk + (size_t)rows * m->num_pdfs));
   float *buf[2] = {ctx->workspace.as<float>(), ctx->workspace.as<float>() + blk};
   float *out = ctx->workspace.as<float>() + 2 * blk;
-  // latency mode (kernels/gemm_bf16x6_lat.hip): every layer's K split into
-  // x6_lat_slices(K, N) slices -- a function of the layer only, so results do
-  // not depend on the row count -- partials in ctx->split_part
-  if (ctx->latency) {
-    size_t part = 0;
-    for (size_t i = 0; i < m->steps.size(); ++i) {
-      const GemmLayer &g = m->steps[i].gemm;
-      const int kpad = i == 0 ? g.kpad : g.nseg * g.din;
-      part = std::max(part, x6_lat_part_floats(rows, g.n, x6_lat_slices(kpad, g.n)));
-    }
-    if (ctx->split_part.bytes < part * sizeof(float)) {
-      CE_HIP(hipStreamSynchronize(ctx->stream));  // the old buffer may still be in use
-      CE_TRY(ctx->split_part.alloc(part * sizeof(float)));
-    }
-  }
   const float *xs = nullptr;
   int px = 0, cur = 0;
   ProfChain chain(ctx);  // every step below is one launch; GEMMs back to back
@@ -1218,14 +1197,7 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
     {
       ProfScope prof(ctx, CE_GPU_PROF_GEMM);
       if (ctx->latency) {
-        // the last layer's reduce fused into the finalize launch
-        const bool defer = last && pend != nullptr && rows <= kX6LatWindow;
-        CE_TRY(launch_gemm_bf16x6_lat(ctx->stream, a, ctx->split_part.as<float>(),
-                                      ctx->split_part.bytes / sizeof(float), !defer));
-        if (defer) {
-          pend->on = true;
-          pend->last = a;
-        }
+        CE_TRY(launch_gemm_bf16x6_lat(ctx->stream, a));
       } else {
         CE_TRY(launch_gemm_bf16x6(ctx->stream, a));
       }
@@ -1461,30 +1433,20 @@ static int run_steps_i8(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, 
   return CE_GPU_OK;
 }
 
-// pend (optional): the caller hands y to finalize_output only, so a
-// latency-mode last layer may leave its reduce to that launch -- returned in
-// *pend, never kept in the context (an error between the two calls leaves
-// nothing behind for a later call to consume)
 static int run_steps(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, int ldx, int rows,
-                     const int *row_map, const uint32_t *row_edge, const float **y, int *ldy,
-                     LatPending *pend = nullptr) {
-  if (pend) pend->on = false;
+                     const int *row_map, const uint32_t *row_edge, const float **y, int *ldy) {
   if (m->int8) return run_steps_i8(ctx, m, x, ldx, rows, row_map, row_edge, y, ldy);
   if (m->gemm == CE_GPU_GEMM_F16X3) return run_steps_x3(ctx, m, x, ldx, rows, row_map, y, ldy);
   if (m->gemm == CE_GPU_GEMM_BF16X6_PLANES) return run_steps_x6(ctx, m, x, ldx, rows, row_map, y, ldy);
   if (m->gemm == CE_GPU_GEMM_BF16X6)
-    return x6_f32in() ? run_steps_x6f(ctx, m, x, ldx, rows, row_map, y, ldy, pend)
+    return x6_f32in() ? run_steps_x6f(ctx, m, x, ldx, rows, row_map, y, ldy)
                       : run_steps_x6(ctx, m, x, ldx, rows, row_map, y, ldy);
   return run_steps_f32(ctx, m, x, ldx, rows, row_map, y, ldy);
 }
 
-// launch_finalize on rows first .. first + rows - 1 of run_steps' output, or
-// the fused reduce + finalize when run_steps left the last reduce pending
-static int finalize_output(ce_gpu_ctx *ctx, const LatPending &pend, const float *y, int ldy, int first, int rows,
-                           int dim, bool log_softmax, const float *log_prior, const int *row_dst, float *out) {
-  if (pend.on)
-    return launch_lat_finalize(ctx->stream, pend.last, ctx->split_part.as<float>(), first, rows, log_softmax,
-                               log_prior, row_dst, out);
+// launch_finalize on rows first .. first + rows - 1 of run_steps' output
+static int finalize_output(ce_gpu_ctx *ctx, const float *y, int ldy, int first, int rows, int dim,
+                           bool log_softmax, const float *log_prior, const int *row_dst, float *out) {
   return launch_finalize(ctx->stream, y + (size_t)first * ldy, ldy, rows, dim, log_softmax, log_prior, row_dst,
                          out);
 }
@@ -1565,10 +1527,9 @@ int ce_gpu_am_forward(ce_gpu_ctx *ctx, const ce_gpu_model *m, const ce_gpu_plan 
     const float *y = nullptr;
     int ldy = 0;
     const uint32_t *row_edge = p->d_row_edge.as<uint32_t>() + c.map_base;
-    LatPending pend;
-    CE_TRY(run_steps(ctx, m, d_feats, m->input_dim, c.rows, row_src, row_edge, &y, &ldy, &pend));
+    CE_TRY(run_steps(ctx, m, d_feats, m->input_dim, c.rows, row_src, row_edge, &y, &ldy));
     ProfScope prof(ctx, CE_GPU_PROF_FINALIZE);
-    CE_TRY(finalize_output(ctx, pend, y, ldy, 0, c.rows, m->num_pdfs, m->final_log_softmax, m->log_prior.as<float>(),
+    CE_TRY(finalize_output(ctx, y, ldy, 0, c.rows, m->num_pdfs, m->final_log_softmax, m->log_prior.as<float>(),
                            row_dst, d_loglik));
   }
   return CE_GPU_OK;
@@ -1615,10 +1576,9 @@ int ce_gpu_nnet_propagate(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *d
   }
   const float *y = nullptr;
   int ldy = 0;
-  LatPending pend;
-  CE_TRY(run_steps(ctx, m, d_in, ld_in, rows, nullptr, nullptr, &y, &ldy, &pend));
+  CE_TRY(run_steps(ctx, m, d_in, ld_in, rows, nullptr, nullptr, &y, &ldy));
   ProfScope prof(ctx, CE_GPU_PROF_FINALIZE);
-  return finalize_output(ctx, pend, y, ldy, m->net_left, out_rows, m->num_pdfs, m->final_log_softmax,
+  return finalize_output(ctx, y, ldy, m->net_left, out_rows, m->num_pdfs, m->final_log_softmax,
                          subtract_prior ? m->log_prior.as<float>() : nullptr, nullptr, d_out);
 }
 
@@ -1673,10 +1633,9 @@ int ce_gpu_nnet_propagate_blocks(ce_gpu_ctx *ctx, const ce_gpu_model *m, const f
   int ldy = 0;
   // blocks are independent: the rows a Splice reads across a block boundary
   // only feed rows that block's Narrow drops
-  LatPending pend;
-  CE_TRY(run_steps(ctx, m, d_in, ld_in, rows, nullptr, d_edge, &y, &ldy, &pend));
+  CE_TRY(run_steps(ctx, m, d_in, ld_in, rows, nullptr, d_edge, &y, &ldy));
   ProfScope prof(ctx, CE_GPU_PROF_FINALIZE);
-  return finalize_output(ctx, pend, y, ldy, 0, rows, m->num_pdfs, m->final_log_softmax,
+  return finalize_output(ctx, y, ldy, 0, rows, m->num_pdfs, m->final_log_softmax,
                          subtract_prior ? m->log_prior.as<float>() : nullptr, d_dst, d_out);
 }
 

@@ -154,24 +154,6 @@ __device__ __forceinline__ float apply_post(float y, float sc, float of, const i
   return y;
 }
 
-// The latency GEMM's split-K reduce (kernels/gemm_bf16x6_lat.hip): the S
-// partials of 4 consecutive outputs at src + s * stride, summed in slice
-// order with sixteen loads in flight.
-__device__ __forceinline__ float4 lat_slice_sum(const float *src, size_t stride, int slices) {
-  float4 sum = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  for (int s0 = 0; s0 < slices; s0 += 16) {
-    float4 v[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u)
-      if (s0 + u < slices) v[u] = *reinterpret_cast<const float4 *>(src + (size_t)(s0 + u) * stride);
-#pragma unroll
-    for (int u = 0; u < 16; ++u)
-      if (s0 + u < slices)
-        sum = s0 + u == 0 ? v[u] : make_float4(sum.x + v[u].x, sum.y + v[u].y, sum.z + v[u].z, sum.w + v[u].w);
-  }
-  return sum;
-}
-
 // Calls f(std::integral_constant<int, MODE>) for the runtime mode.
 template <class F>
 __device__ __forceinline__ void with_post_mode(int mode, F &&f) {
@@ -301,7 +283,6 @@ struct ce_gpu_ctx {
   catears::DevBuf overflow;    // int: an f16x3 split left the fp16 range (ce_gpu_ctx_overflow)
   int latency = 0;             // ce_gpu_ctx_set_latency: split-K GEMMs for small batches
   int fbank_mode = 0;          // ce_gpu_ctx_set_fbank: CE_GPU_FBANK_EXACT / _FAST
-  catears::DevBuf split_part;  // latency mode: GEMM slice partials (grown on demand)
   std::vector<int32_t> h_blk_maps;
   // optional per-class launch timing (ce_gpu_ctx_profile)
   bool profiling = false;
@@ -424,23 +405,11 @@ int gemm_k_align();
 // (y16, plane stride py) or fp32 (y32).
 int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a);
 constexpr int kX6DirUnits = 256;  // gemm_bf16x6d_kernel's unit tile
-// Latency mode v2 (kernels/gemm_bf16x6_lat.hip): K split into
-// x6_lat_slices(kpad, n) slices (a function of K and N only), every slice's
-// fp32 partial stored, then summed in slice order by a reduce kernel that
-// applies bias / ReLU / BatchNorm; needs the weight fragment image (a.wd) and
-// fp32 activations (din a multiple of 8: a segment may end inside a K-tile).
-// part: x6_lat_part_floats(rows, n, slices) floats.  reduce = false (rows <=
-// kX6LatWindow) leaves the partials for launch_lat_finalize.
-constexpr int kX6LatWindow = 1024;
-int x6_lat_slices(int kpad, int n);
-size_t x6_lat_part_floats(int rows, int n, int slices);
-int launch_gemm_bf16x6_lat(hipStream_t s, const X6Gemm &a, float *part, size_t part_floats, bool reduce = true);
-// The last layer's slice reduce fused with launch_finalize: rows first ..
-// first + rows - 1 of the a.m-row partials of a (launch_gemm_bf16x6_lat with
-// reduce = false) summed, + bias, post chain, then (log-softmax) - prior into
-// out (row_dst as launch_finalize) -- the bits of reduce then finalize.
-int launch_lat_finalize(hipStream_t s, const X6Gemm &a, const float *part, int first, int rows, bool log_softmax,
-                        const float *log_prior, const int *row_dst, float *out);
+// Latency mode (kernels/gemm_bf16x6_lat.hip): one launch per layer, 16-unit
+// tiles, K split over a block's four waves (a function of K only) and summed
+// in wave order in LDS, + bias / ReLU / BatchNorm; needs the weight fragment
+// image (a.wd) and fp32 activations (din a multiple of 8).
+int launch_gemm_bf16x6_lat(hipStream_t s, const X6Gemm &a);
 // splice_pad (below) written as three bf16 planes of width po: out row r at
 // out + r * 3 * po.
 int launch_splice_pad_split(hipStream_t s, const float *in, int ld_in, int rows, int din, int nseg, const int *off,

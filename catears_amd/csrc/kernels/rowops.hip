@@ -122,79 +122,6 @@ __global__ __launch_bounds__(256) void finalize_vec_kernel(const float *__restri
   finalize_row_vec<LOGSM>([&](int c) { return xr[c]; }, dim, prior, out + (int64_t)dst * dim, lane);
 }
 
-// finalize_vec_kernel reading the last layer's latency-GEMM partials instead
-// of its output: per 4 outputs the slice sum, + bias, the post chain -- the
-// reduce kernel's arithmetic -- then the same row math.
-struct LatFinalizeArgs {
-  const float *part;
-  int slices, m, first, rows, dim;
-  const float *bias, *bn_scale, *bn_offset;
-  int post[4];
-  int npost;
-  const float *prior;
-  const int *row_dst;
-  float *out;
-};
-
-// One block per row: the 256 threads reduce the row's float4 chunks into LDS
-// (the slice loads of the whole row in flight together), then wave 0 runs the
-// finalize row math on them.
-template <bool LOGSM, int MODE>
-__global__ __launch_bounds__(256) void lat_finalize_kernel(LatFinalizeArgs p) {
-  __shared__ float4 vals[64 * kMaxVecPerLane];
-  const int row = blockIdx.x, tid = threadIdx.x;
-  const int dst = p.row_dst ? p.row_dst[row] : row;
-  if (dst < 0) return;  // block-uniform
-  const float *src = p.part + (size_t)(p.first + row) * p.dim;
-  const size_t stride = (size_t)p.m * p.dim;
-  const int d4 = p.dim >> 2;
-  // every thread's chunks x four slices in flight per step (branch-free:
-  // clamped indices), summed in slice order -- lat_slice_sum's arithmetic
-  constexpr int CPT = 64 * kMaxVecPerLane / 256;
-  float4 sum[CPT], bv[CPT], scv[CPT], ofv[CPT];
-  // bias / BatchNorm chunks first (branch-free, clamped): in flight with the
-  // partials rather than one round trip per chunk after them
-#pragma unroll
-  for (int j = 0; j < CPT; ++j) {
-    const int c = min(tid + 256 * j, d4 - 1);
-    bv[j] = p.bias ? reinterpret_cast<const float4 *>(p.bias)[c] : make_float4(-0.0f, -0.0f, -0.0f, -0.0f);
-    scv[j] = p.npost && p.bn_scale ? reinterpret_cast<const float4 *>(p.bn_scale)[c] : make_float4(1.0f, 1.0f, 1.0f, 1.0f);
-    ofv[j] = p.npost && p.bn_offset ? reinterpret_cast<const float4 *>(p.bn_offset)[c]
-                                    : make_float4(-0.0f, -0.0f, -0.0f, -0.0f);
-  }
-  for (int s0 = 0; s0 < p.slices; s0 += 4) {
-    float4 v[CPT][4];
-#pragma unroll
-    for (int j = 0; j < CPT; ++j)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int c = min(tid + 256 * j, d4 - 1), ss = min(s0 + u, p.slices - 1);
-        v[j][u] = *reinterpret_cast<const float4 *>(src + (size_t)ss * stride + 4 * c);
-      }
-#pragma unroll
-    for (int j = 0; j < CPT; ++j)
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (s0 + u < p.slices)
-          sum[j] = s0 + u == 0 ? v[j][u]
-                               : make_float4(sum[j].x + v[j][u].x, sum[j].y + v[j][u].y, sum[j].z + v[j][u].z,
-                                             sum[j].w + v[j][u].w);
-  }
-#pragma unroll
-  for (int j = 0; j < CPT; ++j) {
-    const int c = tid + 256 * j;
-    if (c >= d4) break;
-    const float4 s4 = sum[j], b = bv[j], sc = scv[j], of = ofv[j];
-    vals[c] = make_float4(apply_post<MODE>(s4.x + b.x, sc.x, of.x, p.post, p.npost),
-                          apply_post<MODE>(s4.y + b.y, sc.y, of.y, p.post, p.npost),
-                          apply_post<MODE>(s4.z + b.z, sc.z, of.z, p.post, p.npost),
-                          apply_post<MODE>(s4.w + b.w, sc.w, of.w, p.post, p.npost));
-  }
-  __syncthreads();
-  if (tid >= 64) return;
-  finalize_row_vec<LOGSM>([&](int c) { return vals[c]; }, p.dim, p.prior, p.out + (int64_t)dst * p.dim, tid);
-}
-
 __global__ __launch_bounds__(256) void rowop_kernel(int kind, float *__restrict__ x, int ldx, int rows,
                                                     int dim, const float *__restrict__ scale,
                                                     const float *__restrict__ offset) {
@@ -298,53 +225,6 @@ int launch_splice(hipStream_t s, int rows, int dim, const float *in, int ld_in, 
   return CE_GPU_OK;
 }
 
-int launch_lat_finalize(hipStream_t s, const X6Gemm &a, const float *part, int first, int rows, bool log_softmax,
-                        const float *log_prior, const int *row_dst, float *out) {
-  if (rows <= 0) return CE_GPU_OK;
-  if (!part || !out || a.n % 4 != 0 || a.n > 4 * 64 * kMaxVecPerLane || first < 0 || first + rows > a.m ||
-      a.npost > 4 ||
-      ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(log_prior) |
-        reinterpret_cast<uintptr_t>(a.bias) | reinterpret_cast<uintptr_t>(a.bn_scale) |
-        reinterpret_cast<uintptr_t>(a.bn_offset)) & 15))
-    return fail(CE_GPU_EINVAL, "lat_finalize: bad geometry");
-  LatFinalizeArgs p;
-  p.part = part;
-  p.slices = x6_lat_slices(a.kpad, a.n);
-  p.m = a.m;
-  p.first = first;
-  p.rows = rows;
-  p.dim = a.n;
-  p.bias = a.bias;
-  p.bn_scale = a.bn_scale;
-  p.bn_offset = a.bn_offset;
-  for (int i = 0; i < 4; ++i) p.post[i] = a.post[i];
-  p.npost = a.npost;
-  p.prior = log_prior;
-  p.row_dst = row_dst;
-  p.out = out;
-  const dim3 grid(rows), block(256);
-  auto go = [&](auto ls) {
-    constexpr bool LS = decltype(ls)::value;
-    switch (post_mode(a.post, a.npost)) {
-      case kPostModeNone: hipLaunchKernelGGL((lat_finalize_kernel<LS, kPostModeNone>), grid, block, 0, s, p); break;
-      case kPostModeRelu: hipLaunchKernelGGL((lat_finalize_kernel<LS, kPostModeRelu>), grid, block, 0, s, p); break;
-      case kPostModeBn: hipLaunchKernelGGL((lat_finalize_kernel<LS, kPostModeBn>), grid, block, 0, s, p); break;
-      case kPostModeReluBn:
-        hipLaunchKernelGGL((lat_finalize_kernel<LS, kPostModeReluBn>), grid, block, 0, s, p);
-        break;
-      case kPostModeBnRelu:
-        hipLaunchKernelGGL((lat_finalize_kernel<LS, kPostModeBnRelu>), grid, block, 0, s, p);
-        break;
-      default: hipLaunchKernelGGL((lat_finalize_kernel<LS, kPostModeGeneric>), grid, block, 0, s, p); break;
-    }
-  };
-  if (log_softmax)
-    go(std::true_type());
-  else
-    go(std::false_type());
-  CE_HIP(hipGetLastError());
-  return CE_GPU_OK;
-}
 
 int launch_finalize(hipStream_t s, const float *x, int ldx, int rows, int dim, bool log_softmax,
                     const float *log_prior, const int *row_dst, float *out) {

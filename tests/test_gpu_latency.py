@@ -1,10 +1,10 @@
-"""Latency mode (ce_gpu_ctx_set_latency, kernels/gemm_bf16x6_lat.hip): the
-fp32 nnet GEMMs split K into slices (x6_lat_slices: a function of K and N
-only, about 256 blocks per 128-row tile block) so a small row block -- the
+"""Latency mode (ce_gpu_ctx_set_latency, kernels/gemm_bf16x6_lat.hip): one
+launch per layer with 16-unit output tiles, so a small row block -- the
 streaming AcousticModel::Process chunk (src/am.cc:115-142) or one utterance
--- spreads over the chip; a reduce kernel sums the slices' partials in slice
-order.  Same bars as the default mode: log-likelihoods within 1e-4 of the
-oracle, bit-identical across row segmentations and batchings, and
+-- spreads over the chip; K is split over each block's four waves (a
+function of K only) and the partial tiles are summed in wave order in LDS.
+Same bars as the default mode: log-likelihoods within 1e-4 of the oracle,
+bit-identical across row segmentations, row-tile shapes and batchings, and
 deterministic run to run (no atomics, no inter-block hand-off)."""
 import numpy as np
 import pytest
@@ -81,7 +81,7 @@ def test_latency_segmentation_and_blocks_exact(torch, G, lctx, oracle, xs_config
 def test_latency_streaming_chunks_deterministic(torch, G, lctx, oracle, s_config):
     """The streaming shape -- 50-frame chunks plus 20 context rows through
     TDNN-S, one call each, 40 calls -- gives identical bits every time (the
-    per-tile tickets re-arm) and matches the oracle."""
+    no state carries between calls) and matches the oracle."""
     from catears_amd import formats
     am = formats.read_am(s_config)
     model = G.Model(lctx, s_config)
@@ -97,9 +97,8 @@ def test_latency_streaming_chunks_deterministic(torch, G, lctx, oracle, s_config
 
 
 def test_latency_long_block_windows(torch, G, lctx, oracle, xs_config):
-    """A block longer than the split-K row window (2048 rows) runs in several
-    launches: the same bits as scoring two overlapping halves separately,
-    and the oracle's values around a window seam."""
+    """A 5000-row block (thousands of row tiles): the same bits as scoring two
+    overlapping halves separately, and the oracle's values in the middle."""
     from catears_amd import formats
     am = formats.read_am(xs_config)
     model = G.Model(lctx, xs_config)
