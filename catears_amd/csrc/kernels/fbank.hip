@@ -40,7 +40,7 @@ constexpr int kFramesPerBlock = 4;  // granularity of the plan's block_utt table
 #define FBANK_WAVES 8
 #endif
 constexpr int kWaves = FBANK_WAVES;  // waves per block (8 frames each)
-constexpr int kBlocksPerCU = 2;      // LDS: 8 x 8 x 1056 B of frame regions + 11.5 KB of tables
+constexpr int kBlocksPerCU = kWaves == 8 ? 2 : 3;  // LDS: kWaves x 8 x 1056 B of frame regions + 11.5 KB of tables
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
