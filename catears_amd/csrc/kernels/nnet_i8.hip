@@ -631,6 +631,155 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_i8_glds_kernel(I8Args 
 }
 
 
+// LDS-DMA through a buffer resource (buffer_load_dwordx4 ... lds): 16 bytes
+// per lane from base + voff into LDS at the wave-uniform lds + 16 * lane.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t r, int8_t *lds, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void *)lds, 16, voff, 0, 0, 0);
+}
+
+// Software-pipelined form of gemm_i8_glds_kernel (the product default):
+// the same tiles, LDS-DMA stages, source swizzle and epilogue, with the loop
+// reordered so that the LDS fragment reads and the MFMAs overlap:
+//   * fragments are double-buffered in registers: k-step s + 1's four
+//     ds_read_b128 are issued before k-step s's four MFMAs, so a read's
+//     latency hides under the MFMAs instead of a lgkmcnt(0) before each step;
+//   * the K-tile hand-off (wait for tile kt + 1's DMA, barrier, refill of
+//     the stage tile kt used, first reads of tile kt + 1) sits after tile
+//     kt's last MFMAs are issued, so the barrier's wait overlaps them.
+// int32 accumulation is exact, so any product order gives the same bits.
+template <int BM, int BN, int STAGES, int WGM, int WGN>
+__global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_i8_pipe_kernel(I8Args p) {
+  static_assert(STAGES == 3, "tile kt + 3 refills tile kt's stage");
+  constexpr int NW = WGM * WGN, BKB = 128, CH = BKB / 16;
+  constexpr int TI = BM / WGM / 32, TJ = BN / WGN / 32;
+  constexpr int RPI = 1024 / BKB;
+  constexpr int NGA = BM * BKB / 1024 / NW, NGB = BN * BKB / 1024 / NW, NG = NGA + NGB;
+  constexpr int STAGE = (BM + BN) * BKB;
+  static_assert(NGA >= 1 && NGB >= 1 && TI >= 1 && TJ >= 1, "tile too small");
+  __shared__ __attribute__((aligned(1024))) int8_t smem[STAGES * STAGE];
+  auto swz = [](int row) { return (row >> 1) & (CH - 1); };
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN, r = lane & 31, h = lane >> 5;
+  int tm, tn;
+  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int lrow = lane / CH, lchunk = lane & (CH - 1);
+  uint32_t boff[NGB];
+#pragma unroll
+  for (int j = 0; j < NGB; ++j) {
+    const int row = (wave * NGB + j) * RPI + lrow;
+    boff[j] = (uint32_t)(min(n0 + row, p.n - 1) * p.kpad + 16 * (lchunk ^ swz(row)));
+  }
+  uint32_t aoff[NGA];
+  int cur_seg = -1;
+  // the DMA as buffer_load ... lds (MUBUF): the compiler counts it in vmcnt
+  // only, so the fragment reads keep exact lgkmcnt waits (a pending
+  // global_load_lds, a FLAT access, makes every LDS wait lgkmcnt(0))
+  const auto ra = buf_rsrc(p.a), rw = buf_rsrc(p.w);
+  auto issue = [&](int kt) {
+    const int k0 = kt * BKB;
+    const int seg = k0 / p.din, col0 = k0 - seg * p.din;
+    if (seg != cur_seg) {
+      cur_seg = seg;
+      const int shift = seg_off(p, seg);
+#pragma unroll
+      for (int i = 0; i < NGA; ++i) {
+        const int row = (wave * NGA + i) * RPI + lrow;
+        int src = m0 + row + shift;
+        src = src < 0 ? 0 : (src > p.m - 1 ? p.m - 1 : src);
+        aoff[i] = (uint32_t)(src * p.lda + 16 * (lchunk ^ swz(row)));
+      }
+    }
+    int8_t *st = smem + (kt % STAGES) * STAGE;
+#pragma unroll
+    for (int i = 0; i < NGA; ++i) buf_lds16(ra, st + (wave * NGA + i) * 1024, aoff[i] + col0);
+#pragma unroll
+    for (int j = 0; j < NGB; ++j) buf_lds16(rw, st + BM * BKB + (wave * NGB + j) * 1024, boff[j] + k0);
+  };
+
+  i32x16 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0;
+
+  const int xr = swz(r) ^ h;  // chunk 2s + h -> (2s) ^ xr
+  const int a_row = (wm * TI * 32 + r) * BKB, b_row = BM * BKB + (wn * TJ * 32 + r) * BKB;
+  const int ktiles = p.kpad / BKB;
+  i32x4 fa[2][TI], fb[2][TJ];
+  auto read = [&](int kt, int s, int buf) {
+    const int8_t *st = smem + (kt % STAGES) * STAGE;
+    const int ch = ((2 * s) ^ xr) * 16;
+#pragma unroll
+    for (int i = 0; i < TI; ++i) fa[buf][i] = *reinterpret_cast<const i32x4 *>(st + a_row + i * 32 * BKB + ch);
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) fb[buf][j] = *reinterpret_cast<const i32x4 *>(st + b_row + j * 32 * BKB + ch);
+  };
+  auto mma = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[buf][i], fb[buf][j], acc[i][j], 0, 0, 0);
+  };
+  // tile kt has landed once at most the newer tiles' groups are outstanding
+  auto wait_tile = [&](int newer) {
+    if (newer >= 2)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NG) : "memory");
+    else if (newer == 1)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NG) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  for (int t = 0; t < STAGES - 1 && t < ktiles; ++t) issue(t);
+  wait_tile(min(ktiles - 1, STAGES - 2));
+  __builtin_amdgcn_s_barrier();
+  if (STAGES - 1 < ktiles) issue(STAGES - 1);
+  read(0, 0, 0);
+  for (int kt = 0; kt < ktiles; ++kt) {
+    // k-steps 0..2: the next step's reads, then this step's MFMAs
+    read(kt, 1, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(0);
+    __builtin_amdgcn_sched_barrier(0);
+    read(kt, 2, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(1);
+    __builtin_amdgcn_sched_barrier(0);
+    read(kt, 3, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(0);
+    __builtin_amdgcn_sched_barrier(0);
+    // k-step 3's MFMAs first, then the hand-off to tile kt + 1 under them
+    mma(1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 1 < ktiles) {
+      // newer tiles than kt + 1 already issued: kt + 2 if it exists
+      wait_tile(kt + 2 < ktiles ? 1 : 0);
+      __builtin_amdgcn_s_barrier();  // every wave is past its reads of tile kt's stage
+      if (kt + STAGES < ktiles) issue(kt + STAGES);
+      read(kt + 1, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+
+  constexpr bool kVecFits = NW * 32 * (TJ * 32 + 8) * 4 + BM * 4 <= STAGES * STAGE;  // slabs + row sums
+  if (kVecFits && p.vec_epi)
+    i8_epilogue_v<TI, TJ, BM, 64 * NW>(p, acc, m0, wm * TI * 32, n0 + wn * TJ * 32, r, h,
+                                       reinterpret_cast<char *>(smem));
+  else
+    i8_epilogue<TI, TJ, BM, 64 * NW>(p, acc, m0, wm * TI * 32, n0 + wn * TJ * 32, r, h,
+                                     reinterpret_cast<uint32_t *>(smem));
+}
+
 // Branch-free form of gemm_i8_glds_kernel with three stages and the DMA two
 // K-tiles ahead (the structure of gemm_bf16x6q_kernel): step kt reads stage
 // kt % 3 (four k-steps), drains its LDS reads (lgkmcnt(0)), retires its own
@@ -921,7 +1070,7 @@ int launch_i8_gemm(hipStream_t s, const I8Layer &L, const int8_t *a, int lda, in
   p.vec_epi = vec_epi && L.n % 4 == 0 && ldy % 4 == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0;
   static const int use_glds = [] {
     const char *e = getenv("CATEARS_I8_GEMM");
-    return e ? atoi(e) : 15;  // measured best on TDNN-S, frame batch 8192 (tools/i8_sweep.sh)
+    return e ? atoi(e) : 16;  // measured best on TDNN-S, frame batch 8192 (tools/i8_sweep.sh)
   }();
   if (use_glds && p.kpad % 128 == 0 && p.din % 128 == 0 && lda % 16 == 0) {
     auto go = [&](auto kern, int bm, int bn, int threads = 256) {
@@ -938,6 +1087,8 @@ int launch_i8_gemm(hipStream_t s, const I8Layer &L, const int8_t *a, int lda, in
       // (the loop waits on L2 / MALL fetches, 43 % of wave cycles parked, MFMA
       // busy ~20 %); 9 (128 tiles) leaves half the CUs idle when alone.
       case 15: go(gemm_i8_glds_kernel<256, 128, 3, 4, 2>, 256, 128, 512); break;
+      // 16: 15's tiles with the loop software-pipelined (gemm_i8_pipe_kernel)
+      case 16: go(gemm_i8_pipe_kernel<256, 128, 3, 4, 2>, 256, 128, 512); break;
 #ifdef CATEARS_EXPERIMENTS  // tools/i8_sweep.sh
       case 2: go(gemm_i8_glds_kernel<128, 128, 3>, 128, 128); break;
       case 3: go(gemm_i8_glds_kernel<128, 128, 4>, 128, 128); break;
@@ -986,7 +1137,7 @@ int launch_i8_gemm(hipStream_t s, const I8Layer &L, const int8_t *a, int lda, in
 #endif
       default:
         return fail(CE_GPU_EINVAL, "CATEARS_I8_GEMM=" + std::to_string(use_glds) +
-                                       " is not a kernel of this build (product: 15, or 0 for the register-staged "
+                                       " is not a kernel of this build (product: 16, 15, or 0 for the register-staged "
                                        "fallback; others need `make EXPERIMENTS=1`)");
     }
     CE_HIP(hipGetLastError());
