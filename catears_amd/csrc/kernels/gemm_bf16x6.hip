@@ -786,6 +786,104 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
   x6_epilogue<TW, TF, false>(p, acc, n0 + ww * TW * 16, f0 + frow, lane);
 }
 
+// Register-direct schedule (variant 400): both operands go straight from
+// L2 / L1 to registers -- the weights from the MFMA-fragment image as in
+// gemm_bf16x6d_kernel, the activations as each lane's 8 consecutive floats of
+// one row (the B-fragment layout of v_mfma_f32_16x16x32_bf16), split into
+// their three bf16 planes in registers by the wave that multiplies them.  No
+// LDS, no barrier: every wave runs its K loop at its own pace, with the next
+// K-tile's loads in flight under this one's MFMAs.  The price is each
+// activation fragment fetched by the WGW waves along the units (from L1 after
+// the first) and split by each of them.  Products and their order per
+// element are gemm_bf16x6d_kernel's (a0b0, a0b1, a1b0, a1b1, a0b2, a2b0 per
+// K-tile, K-tiles in order): bit-identical results.
+template <class C>
+__global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6r_kernel(X6Args p) {
+  constexpr int TW = C::TW, TF = C::TF;
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef const __attribute__((address_space(1))) f32x4v gvec;
+  typedef const __attribute__((address_space(1))) bf16x8 gfrag;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ww = wave / C::WGF, wf = wave % C::WGF;
+  int tm, tn;
+  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
+  const int f0 = tm * C::BF + wf * TF * 16, n0 = tn * C::BW;
+  const int ktiles = p.kpad / 32;
+  gfrag *wb[TW];
+#pragma unroll
+  for (int i = 0; i < TW; ++i)
+    wb[i] = (gfrag *)(p.wd + ((size_t)((n0 >> 4) + ww * TW + i) * p.wd_kt * 3 * 64 + lane) * 8);
+  // the lane's rows (frame f0 + 16 j + (lane & 15)) and k chunk (8 (lane >> 4))
+  int xrow[TF];
+#pragma unroll
+  for (int j = 0; j < TF; ++j) xrow[j] = f0 + 16 * j + (lane & 15);
+  bf16x8 a[2][3][TW];
+  f32x4v x[2][TF][2];
+  auto load = [&](int kt, int buf) {
+    kt = min(kt, ktiles - 1);  // the tail's prefetch refetches the last tile (unused)
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+      for (int i = 0; i < TW; ++i) a[buf][pl][i] = wb[i][(kt * 3 + pl) * 64];
+    const int k0 = kt * 32;
+    const int seg = k0 / p.din, col = k0 - seg * p.din + 8 * (lane >> 4);
+    const int shift = (int)(signed char)(p.off_packed >> (8 * seg));
+#pragma unroll
+    for (int j = 0; j < TF; ++j) {
+      const int src = clampi(xrow[j] + shift, 0, p.m - 1);
+      gvec *xp = (gvec *)(p.xf + (size_t)src * p.ldx + col);
+      x[buf][j][0] = xp[0];
+      x[buf][j][1] = xp[1];
+    }
+  };
+  f32x4 acc[TW][TF];
+#pragma unroll
+  for (int i = 0; i < TW; ++i)
+#pragma unroll
+    for (int j = 0; j < TF; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  auto compute = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < TF; ++j) {
+      const f32x4v v0 = x[buf][j][0], v1 = x[buf][j][1];
+      const Planes2 q0 = split3_pair(v0.x, v0.y), q1 = split3_pair(v0.z, v0.w);
+      const Planes2 q2 = split3_pair(v1.x, v1.y), q3 = split3_pair(v1.z, v1.w);
+      const bf16x8 b0 = __builtin_bit_cast(bf16x8, u32x4{q0.h, q1.h, q2.h, q3.h});
+      const bf16x8 b1 = __builtin_bit_cast(bf16x8, u32x4{q0.m, q1.m, q2.m, q3.m});
+      const bf16x8 b2 = __builtin_bit_cast(bf16x8, u32x4{q0.l, q1.l, q2.l, q3.l});
+      // each product over the TW accumulators before the next: TW
+      // independent MFMAs between an accumulator's dependent ones
+#pragma unroll
+      for (int i = 0; i < TW; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[buf][0][i], b0, acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TW; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[buf][0][i], b1, acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TW; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[buf][1][i], b0, acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TW; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[buf][1][i], b1, acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TW; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[buf][0][i], b2, acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TW; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[buf][2][i], b0, acc[i][j], 0, 0, 0);
+    }
+  };
+  load(0, 0);
+  int kt = 0;
+  for (; kt + 1 < ktiles; kt += 2) {
+    load(kt + 1, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(0);
+    __builtin_amdgcn_sched_barrier(0);
+    load(kt + 2, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(1);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (kt < ktiles) compute(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail prefetch
+  x6_epilogue<TW, TF, false>(p, acc, n0 + ww * TW * 16, f0, lane);
+}
+
 // Warp-specialised fp32-in schedule: the block is C::NW MFMA waves plus
 // NPV producer waves.  The producers do all the global loads, splits and
 // plane writes of tile kt+1 while the MFMA waves read and multiply tile kt,
@@ -984,6 +1082,16 @@ int launch_f(hipStream_t s, X6Args p) {
 }
 
 template <class C>
+int launch_r(hipStream_t s, X6Args p) {
+  p.tiles_n = (p.n + C::BW - 1) / C::BW;
+  p.tiles_m = (p.m + C::BF - 1) / C::BF;
+  dim3 grid(p.tiles_m * p.tiles_n), block(C::NT);
+  hipLaunchKernelGGL((gemm_bf16x6r_kernel<C>), grid, block, 0, s, p);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
+template <class C>
 int launch_d(hipStream_t s, X6Args p) {
   p.tiles_n = (p.n + C::BW - 1) / C::BW;
   p.tiles_m = (p.m + C::BF - 1) / C::BF;
@@ -1100,6 +1208,10 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
         return launch_f<X6Cfg<128, 256, 2, 4, 2>, 8>(s, p);
       case 40:  // 128 x 128 tiles: fills all CUs on a 1024-wide layer (one batch at a time on an idle GPU)
         return launch_f<X6Cfg<128, 128, 4, 2, 2>>(s, p);
+      case 400:  // register-direct: both operands straight to registers, no LDS
+        if (!a.wd || a.wd_kt * 32 < a.kpad || (reinterpret_cast<uintptr_t>(a.wd) & 15))
+          return fail(CE_GPU_EINVAL, "variant 400 needs the weight fragment image");
+        return launch_r<X6Cfg<kX6DirUnits, 128, 4, 2, 2>>(s, p);
       case 200:  // warp-specialised: 4 MFMA waves (64 x 64 each) + 4 producer waves
         return launch_ws<X6Cfg<128, 128, 2, 2, 2>, 4>(s, p);
 #ifdef CATEARS_EXPERIMENTS
@@ -1140,7 +1252,7 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
 #endif
       default:
         return fail(CE_GPU_EINVAL, "CATEARS_X6_VARIANT=" + std::to_string(x6_variant()) +
-                                       " is not a schedule of this build (product: 0, 300, 160, 40, 200; others need "
+                                       " is not a schedule of this build (product: 0, 300, 400, 160, 40, 200; others need "
                                        "`make EXPERIMENTS=1`)");
     }
   }
