@@ -666,6 +666,7 @@ def verify_serial(args, kept, ctx, model, plan, pcm, gstats, U, pool):
 
     from catears_amd import gpu
     torch.cuda.synchronize()
+    ctx.set_fbank(args.fbank)  # the front contexts' fbank mode (the re-score runs on one context)
     raw = torch.empty_like(kept[0][0])
     norm = torch.empty_like(raw) if gstats is not None else raw
     out = torch.empty((plan.total_frames, model.num_pdfs), dtype=torch.float32, device="cuda")

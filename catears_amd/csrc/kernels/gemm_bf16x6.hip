@@ -786,6 +786,7 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
   x6_epilogue<TW, TF, false>(p, acc, n0 + ww * TW * 16, f0 + frow, lane);
 }
 
+#ifdef CATEARS_EXPERIMENTS
 // Register-direct schedule (variant 400): both operands go straight from
 // L2 / L1 to registers -- the weights from the MFMA-fragment image as in
 // gemm_bf16x6d_kernel, the activations as each lane's 8 consecutive floats of
@@ -883,6 +884,8 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6r_kernel(X6Args p) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail prefetch
   x6_epilogue<TW, TF, false>(p, acc, n0 + ww * TW * 16, f0, lane);
 }
+
+#endif  // CATEARS_EXPERIMENTS
 
 // Warp-specialised fp32-in schedule: the block is C::NW MFMA waves plus
 // NPV producer waves.  The producers do all the global loads, splits and
@@ -1081,6 +1084,7 @@ int launch_f(hipStream_t s, X6Args p) {
   return CE_GPU_OK;
 }
 
+#ifdef CATEARS_EXPERIMENTS
 template <class C>
 int launch_r(hipStream_t s, X6Args p) {
   p.tiles_n = (p.n + C::BW - 1) / C::BW;
@@ -1090,6 +1094,7 @@ int launch_r(hipStream_t s, X6Args p) {
   CE_HIP(hipGetLastError());
   return CE_GPU_OK;
 }
+#endif
 
 template <class C>
 int launch_d(hipStream_t s, X6Args p) {
@@ -1208,13 +1213,17 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
         return launch_f<X6Cfg<128, 256, 2, 4, 2>, 8>(s, p);
       case 40:  // 128 x 128 tiles: fills all CUs on a 1024-wide layer (one batch at a time on an idle GPU)
         return launch_f<X6Cfg<128, 128, 4, 2, 2>>(s, p);
-      case 400:  // register-direct: both operands straight to registers, no LDS
-        if (!a.wd || a.wd_kt * 32 < a.kpad || (reinterpret_cast<uintptr_t>(a.wd) & 15))
-          return fail(CE_GPU_EINVAL, "variant 400 needs the weight fragment image");
-        return launch_r<X6Cfg<kX6DirUnits, 128, 4, 2, 2>>(s, p);
       case 200:  // warp-specialised: 4 MFMA waves (64 x 64 each) + 4 producer waves
         return launch_ws<X6Cfg<128, 128, 2, 2, 2>, 4>(s, p);
 #ifdef CATEARS_EXPERIMENTS
+      // 400: register-direct, both operands straight to registers, no LDS
+      // (bit-identical; C3 4.50-4.52 vs 5.67-5.69 M frames/s, serial layers
+      // 0.183 vs 0.127 ms: the activation fragments fetched by all four waves
+      // along the units and split by each make it L1-bound)
+      case 400:
+        if (!a.wd || a.wd_kt * 32 < a.kpad || (reinterpret_cast<uintptr_t>(a.wd) & 15))
+          return fail(CE_GPU_EINVAL, "variant 400 needs the weight fragment image");
+        return launch_r<X6Cfg<kX6DirUnits, 128, 4, 2, 2>>(s, p);
       case 302:  // direct weights, 128 x 128 tiles (twice the blocks of 300)
         if (!a.wd) return fail(CE_GPU_EINVAL, "variant 302 needs the weight fragment image");
         return launch_d<X6Cfg<128, 128, 2, 4, 2>>(s, p);
@@ -1252,7 +1261,7 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
 #endif
       default:
         return fail(CE_GPU_EINVAL, "CATEARS_X6_VARIANT=" + std::to_string(x6_variant()) +
-                                       " is not a schedule of this build (product: 0, 300, 400, 160, 40, 200; others need "
+                                       " is not a schedule of this build (product: 0, 300, 160, 40, 200; others need "
                                        "`make EXPERIMENTS=1`)");
     }
   }

@@ -621,13 +621,17 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_i8_glds_kernel(I8Args 
     p.y[(int64_t)blockIdx.x * 64 * NW + tid] = (float)t;
     return;
   }
-  constexpr bool kVecFits = NW * 32 * (TJ * 32 + 8) * 4 + BM * 4 <= STAGES * STAGE;  // slabs + row sums
-  if (kVecFits && p.vec_epi)
-    i8_epilogue_v<TI, TJ, BM, 64 * NW>(p, acc, m0, wm * TI * 32, n0 + wn * TJ * 32, r, h,
-                                       reinterpret_cast<char *>(smem));
-  else
-    i8_epilogue<TI, TJ, BM, 64 * NW>(p, acc, m0, wm * TI * 32, n0 + wn * TJ * 32, r, h,
-                                     reinterpret_cast<uint32_t *>(smem));
+  // slabs + row sums in the stages; one 64-row held-row mask per wave
+  constexpr bool kVecFits = TI == 2 && NW * 32 * (TJ * 32 + 8) * 4 + BM * 4 <= STAGES * STAGE;
+  if constexpr (kVecFits) {
+    if (p.vec_epi) {
+      i8_epilogue_v<TI, TJ, BM, 64 * NW>(p, acc, m0, wm * TI * 32, n0 + wn * TJ * 32, r, h,
+                                         reinterpret_cast<char *>(smem));
+      return;
+    }
+  }
+  i8_epilogue<TI, TJ, BM, 64 * NW>(p, acc, m0, wm * TI * 32, n0 + wn * TJ * 32, r, h,
+                                   reinterpret_cast<uint32_t *>(smem));
 }
 
 
@@ -771,13 +775,17 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_i8_pipe_kernel(I8Args 
     __builtin_amdgcn_sched_barrier(0);
   }
 
-  constexpr bool kVecFits = NW * 32 * (TJ * 32 + 8) * 4 + BM * 4 <= STAGES * STAGE;  // slabs + row sums
-  if (kVecFits && p.vec_epi)
-    i8_epilogue_v<TI, TJ, BM, 64 * NW>(p, acc, m0, wm * TI * 32, n0 + wn * TJ * 32, r, h,
-                                       reinterpret_cast<char *>(smem));
-  else
-    i8_epilogue<TI, TJ, BM, 64 * NW>(p, acc, m0, wm * TI * 32, n0 + wn * TJ * 32, r, h,
-                                     reinterpret_cast<uint32_t *>(smem));
+  // slabs + row sums in the stages; one 64-row held-row mask per wave
+  constexpr bool kVecFits = TI == 2 && NW * 32 * (TJ * 32 + 8) * 4 + BM * 4 <= STAGES * STAGE;
+  if constexpr (kVecFits) {
+    if (p.vec_epi) {
+      i8_epilogue_v<TI, TJ, BM, 64 * NW>(p, acc, m0, wm * TI * 32, n0 + wn * TJ * 32, r, h,
+                                         reinterpret_cast<char *>(smem));
+      return;
+    }
+  }
+  i8_epilogue<TI, TJ, BM, 64 * NW>(p, acc, m0, wm * TI * 32, n0 + wn * TJ * 32, r, h,
+                                   reinterpret_cast<uint32_t *>(smem));
 }
 
 // Branch-free form of gemm_i8_glds_kernel with three stages and the DMA two
