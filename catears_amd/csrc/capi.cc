@@ -1128,12 +1128,30 @@ static int run_steps_f32(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
 // the plane kernels (tools/ab.sh).
 // Default; CATEARS_X6_F32IN=0 selects the plane-operand kernels
 // (run_steps_x6: planes written by each epilogue, bit-identical results).
+static int x6_variant_env() {
+  static const int v = [] {
+    const char *e = getenv("CATEARS_X6_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 static bool x6_f32in() {
   static const bool v = [] {
     const char *e = getenv("CATEARS_X6_F32IN");
     return !e || atoi(e) != 0;
   }();
   return v;
+}
+
+// CATEARS_X6_FIRST=0 keeps the round-3 splice_pad launch before the first
+// layer's throughput GEMM (bit-identical; the default gathers in its loader)
+static bool x6_first_direct() {
+  static const bool v = [] {
+    const char *e = getenv("CATEARS_X6_FIRST");
+    return !e || atoi(e) != 0;
+  }();
+  return v && (x6_variant_env() == 0 || x6_variant_env() == 300);
 }
 
 static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, int ldx, int rows,
@@ -1152,9 +1170,11 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
     const GemmLayer &g = m->steps[i].gemm;
     const bool last = i + 1 == m->steps.size();
     X6Gemm a;
-    // the latency kernel splices the caller's rows itself (din % 8 == 0)
-    const bool lat_direct = ctx->latency && i == 0 && g.din % 8 == 0 && ldx % 4 == 0 &&
-                            (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+    // the latency kernel and the default direct-weight kernel splice the
+    // caller's rows themselves (din % 8 == 0): no splice_pad launch
+    const bool lat_direct = i == 0 && g.din % 8 == 0 && ldx % 4 == 0 &&
+                            (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+                            (ctx->latency || (g.wdir.ptr && x6_first_direct()));
     if (lat_direct) {
       xs = x;
       px = ldx;

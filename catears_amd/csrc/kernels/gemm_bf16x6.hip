@@ -70,6 +70,11 @@ struct X6Args {
   int tiles_m, tiles_n, group;
   const uint16_t *wd;  // weights as MFMA A fragments (gemm_bf16x6d_kernel), see X6Gemm::wd
   int wd_kt;           // K-tiles per 16-unit block in that image
+  // first layer read straight from the caller's rows (gemm_bf16x6d_kernel
+  // FIRST): nseg segments of din (a multiple of 8) floats, segment s of
+  // packed row r = xf row row_map[clamp(r + off[s])]; zeros past them
+  const int *row_map;
+  int nseg;
 };
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
@@ -654,7 +659,7 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
 //   WAR: activation stage (kt+1) % 2 was last read in tile kt-1, before the
 //        barrier that closed it; RAW: its writes precede the barrier that
 //        closes tile kt.
-template <class C>
+template <class C, bool FIRST = false>
 __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
   constexpr int BF = C::BF, TW = C::TW, TF = C::TF, NT = C::NT;
   constexpr int RPP = NT / 4;  // activation rows per pass (4 threads x 32 B per row)
@@ -689,13 +694,27 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
   auto load_x = [&](int kt, int r) {
     kt = min(kt, ktiles - 1);
     const int k0 = kt * 32;
-    const int seg = k0 / p.din, col0 = k0 - seg * p.din;
-    const int shift = (int)(signed char)(p.off_packed >> (8 * seg));
-    gvec *xb = (gvec *)(p.xf + col0 + 8 * pch);
-    const int src = clampi(f0 + prow + shift, 0, p.m - 1);
-    const uint32_t o = (uint32_t)(src * p.ldx) / 4;
-    rx0[r] = xb[o];
-    rx1[r] = xb[o + 1];
+    if constexpr (FIRST) {
+      // the splice (5 x 40 for TDNN-S) and row_map gather of splice_pad,
+      // per thread: its 8 k lie in one segment; past the segments, zeros
+      // (read from column 0 of a valid row)
+      const int k = k0 + 8 * pch, seg = k / p.din, segc = min(seg, p.nseg - 1);
+      const int shift = (int)(signed char)(p.off_packed >> (8 * segc));
+      int src = clampi(clampi(f0 + prow, 0, p.m - 1) + shift, 0, p.m - 1);
+      if (p.row_map) src = p.row_map[src];
+      gvec *xb = (gvec *)(p.xf + (size_t)src * p.ldx + (seg < p.nseg ? k - segc * p.din : 0));
+      rx0[r] = xb[0];
+      rx1[r] = xb[1];
+      if (seg >= p.nseg) rx0[r] = rx1[r] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+    } else {
+      const int seg = k0 / p.din, col0 = k0 - seg * p.din;
+      const int shift = (int)(signed char)(p.off_packed >> (8 * seg));
+      gvec *xb = (gvec *)(p.xf + col0 + 8 * pch);
+      const int src = clampi(f0 + prow + shift, 0, p.m - 1);
+      const uint32_t o = (uint32_t)(src * p.ldx) / 4;
+      rx0[r] = xb[o];
+      rx1[r] = xb[o + 1];
+    }
   };
   auto put = [&](char *st, int r) {
     const Planes2 q0 = split3_pair(rx0[r].x, rx0[r].y), q1 = split3_pair(rx0[r].z, rx0[r].w);
@@ -1101,7 +1120,10 @@ int launch_d(hipStream_t s, X6Args p) {
   p.tiles_n = (p.n + C::BW - 1) / C::BW;
   p.tiles_m = (p.m + C::BF - 1) / C::BF;
   dim3 grid(p.tiles_m * p.tiles_n), block(C::NT);
-  hipLaunchKernelGGL((gemm_bf16x6d_kernel<C>), grid, block, 0, s, p);
+  if (p.row_map || p.nseg > 1 && p.din % 32 != 0)
+    hipLaunchKernelGGL((gemm_bf16x6d_kernel<C, true>), grid, block, 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_bf16x6d_kernel<C>), grid, block, 0, s, p);
   CE_HIP(hipGetLastError());
   return CE_GPU_OK;
 }
@@ -1138,8 +1160,14 @@ int x6_variant() {
 
 int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
   if (a.m <= 0 || a.n <= 0) return CE_GPU_OK;
-  if (a.kpad % 32 != 0 || a.din % 32 != 0 || a.nseg < 1 || a.nseg > 8 || a.nseg * a.din > a.kpad)
+  // a first layer gathered in the loader (row_map, or segments that are not
+  // whole K-tiles) needs the direct-weight kernel and din % 8 == 0
+  const bool first = a.row_map != nullptr || a.din % 32 != 0;
+  if (a.kpad % 32 != 0 || a.din % (first ? 8 : 32) != 0 || a.din <= 0 || a.nseg < 1 || a.nseg > 8 ||
+      a.nseg * a.din > a.kpad)
     return fail(CE_GPU_EINVAL, "gemm_bf16x6: bad K geometry");
+  if (first && (!a.xf || !a.wd || (x6_variant() != 0 && x6_variant() != 300)))
+    return fail(CE_GPU_EINVAL, "gemm_bf16x6: a gathered first layer needs fp32 input and the direct-weight kernel");
   if (a.n % 4 != 0 || a.ldy % 4 != 0 || (a.y16 && a.py % 4 != 0))
     return fail(CE_GPU_EINVAL, "gemm_bf16x6: output width must be a multiple of 4");
   const bool f32in = a.xf != nullptr;
@@ -1179,6 +1207,8 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
   p.n = a.n;
   p.kpad = a.kpad;
   p.din = a.din;
+  p.nseg = a.nseg;
+  p.row_map = a.row_map;
   p.off_packed = 0;
   for (int i = 0; i < a.nseg; ++i) {
     if (a.off[i] < -128 || a.off[i] > 127) return fail(CE_GPU_ENOTSUP, "gemm_bf16x6: splice offset beyond +-127");

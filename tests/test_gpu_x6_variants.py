@@ -29,15 +29,15 @@ np.save(sys.argv[2], out)
 """
 
 
-def _child(variant, cfg, path):
-    env = dict(os.environ, CATEARS_X6_VARIANT=str(variant), PYTHONPATH=ROOT)
+def _child(variant, cfg, path, **extra_env):
+    env = dict(os.environ, CATEARS_X6_VARIANT=str(variant), PYTHONPATH=ROOT, **extra_env)
     env.pop("CATEARS_HIP_LIB", None)
     return subprocess.run([sys.executable, "-c", CHILD, cfg, str(path)], env=env, capture_output=True, text=True,
                           timeout=300, cwd=ROOT)
 
 
-def _run(variant, cfg, path):
-    r = _child(variant, cfg, path)
+def _run(variant, cfg, path, **extra_env):
+    r = _child(variant, cfg, path, **extra_env)
     assert r.returncode == 0, r.stderr[-3000:]
     return np.load(path).view(np.uint32)
 
@@ -48,6 +48,10 @@ def test_x6_variants_bit_identical(tmp_path, s_config):
     for v in (40, 200):
         got = _run(v, s_config, tmp_path / f"v{v}.npy")
         assert np.array_equal(got, base), f"variant {v} differs from the default"
+    # the first layer's splice + row gather in the default kernel's loader
+    # against the round-3 splice_pad launch before it (CATEARS_X6_FIRST=0)
+    padded = _run(0, s_config, tmp_path / "pad.npy", CATEARS_X6_FIRST="0")
+    assert np.array_equal(padded, base), "the gathered first layer differs from splice_pad"
 
 
 def test_unknown_variant_fails_loudly(tmp_path, s_config):
