@@ -184,7 +184,9 @@ def cpu_baseline(conf, n_utts, seconds, threads, min_wall):
 ROOFLINE_KERNEL = "gemm_f32_glds_kernel<catears::Cfg<128, 64, 32, 2, 2>, 2, false>"
 # split-plane hidden layers (split output), the default variants
 SPLIT_ROOFLINE_KERNEL = {
-    "bf16x6": "gemm_bf16x6d_kernel<catears::X6Cfg<256, 128, 4, 2, 2> >",  # CATEARS_X6_VARIANT 0 = 300
+    # CATEARS_X6_VARIANT 0 = 300; both instantiations (first layer gathered
+    # in the loader, and layers 2-7)
+    "bf16x6": "gemm_bf16x6d_kernel<catears::X6Cfg<256, 128, 4, 2, 2>*",
     "bf16x6_160": "gemm_bf16x6f_kernel<catears::X6Cfg<128, 256, 2, 4, 2>, 8, 0, false>",
     "bf16x6p": "gemm_bf16x6q_kernel<catears::X6Cfg<128, 128, 4, 2, 3>, true, 0>",
     "f16x3": "gemm_f16x3_kernel<catears::X3Cfg<128, 128, 2, 4, 2, 64>, true>",
@@ -199,7 +201,7 @@ SPLIT_DTYPE = {
              "significant bits, 3 MFMA products in 2 fp32 accumulators; error vs oracle at the fp32-MFMA "
              "path's level, tests/test_gpu_parity.py)",
 }
-I8_ROOFLINE_KERNEL = "gemm_i8_glds_kernel<256, 128, 3, 4, 2, 128, 0>"  # CATEARS_I8_GEMM default (nnet_i8.hip)
+I8_ROOFLINE_KERNEL = "gemm_i8_pipe_kernel<256, 128, 3, 4, 2>"  # CATEARS_I8_GEMM default 16 (nnet_i8.hip)
 
 
 def gemm_algorithmic_bytes(rows, layers=((3072, 1024),) * 4 + ((1024, 1024), (1024, 3456))):
@@ -225,6 +227,17 @@ def split_algorithmic_bytes(rows, eb, layers=((256, 1024),) + ((3072, 1024),) * 
     return tot / len(layers)
 
 
+def kernel_match(name, kernel):
+    """A profiled kernel name is `kernel`, or, for a `kernel` ending in '*',
+    any instantiation that begins with it (e.g. every value of a trailing
+    template argument)."""
+    name = name.replace("catears::", "")
+    kernel = kernel.replace("catears::", "")
+    if kernel.endswith("*"):
+        return kernel[:-1] in name
+    return name.endswith(kernel)
+
+
 def pmc_traffic(kernel, workload="c3"):
     """Per-launch HBM bytes of `kernel` from the newest committed PMC summary
     (tools/pmc_traffic.py over rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes
@@ -236,10 +249,13 @@ def pmc_traffic(kernel, workload="c3"):
     if not files:
         return None, None
     data = json.load(open(files[-1]))
-    for name, v in data.get("kernels", {}).items():
-        if name.endswith(kernel):
-            return v["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
-    return None, None
+    # every instantiation of the kernel (the default GEMM's first-layer form
+    # is its own), weighted by dispatches: bytes per launch over all layers
+    hits = [v for name, v in data.get("kernels", {}).items() if kernel_match(name, kernel)]
+    if not hits:
+        return None, None
+    n = sum(v["dispatches"] for v in hits)
+    return round(sum(v["hbm_bytes_per_launch"] * v["dispatches"] for v in hits) / n), os.path.relpath(files[-1], ROOT)
 
 
 def pmc_mfma(kernel, workload="c3"):
@@ -255,9 +271,12 @@ def pmc_mfma(kernel, workload="c3"):
     if not files:
         return None
     data = json.load(open(files[-1]))
-    for name, v in data.get("kernels", {}).items():
-        if name.endswith(kernel):
-            return {"chip": v["mfma_util_chip"], "active_cus": v["mfma_util_active_cus"],
+    hits = [v for name, v in data.get("kernels", {}).items() if kernel_match(name, kernel)]
+    if hits:
+        n = sum(v["dispatches"] for v in hits)
+        avg = lambda key: round(sum(v[key] * v["dispatches"] for v in hits) / n, 4)
+        if True:
+            return {"chip": avg("mfma_util_chip"), "active_cus": avg("mfma_util_active_cus"),
                     "source": os.path.relpath(files[-1], ROOT),
                     "definition": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 x SIMDs), serial run: chip = "
                                   "1024 SIMDs, active_cus = 4 x the CUs the grid occupies"}
@@ -383,7 +402,7 @@ def main_c2(args):
     if iv:
         avg_ms = sum(b - a for a, b in iv) / len(iv)
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-        kname = ("fbank_fast_kernel" if args.fbank == "fast" else "fbank_kernel") + ("<short>" if s16 else "<float>")
+        kname = ("fbank_fast_kernel" if args.fbank == "fast" else "fbank_kernel") + ("<short*" if s16 else "<float*")
         traffic, src = pmc_traffic(kname, "c2")
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,

@@ -691,6 +691,19 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
     for (int i = 0; i < TW; ++i) dst[i] = wb[i][(kt * 3 + pl) * 64];
   };
   f32x4v rx0[2], rx1[2];  // activation row chunks of tiles kt+1 / kt+2 (by parity)
+  // FIRST: every (segment, tile row)'s source row, gathered once into LDS
+  // (a row_map load per K-tile would put a dependent global load in front of
+  // every activation load; eight values in registers went to scratch)
+  __shared__ int src_tab[FIRST ? 8 * BF : 1];
+  if constexpr (FIRST) {
+    for (int i = tid; i < 8 * BF; i += NT) {
+      const int sg = i / BF, row = i % BF;
+      const int shift = (int)(signed char)(p.off_packed >> (8 * min(sg, p.nseg - 1)));
+      const int src = clampi(clampi(f0 + row, 0, p.m - 1) + shift, 0, p.m - 1);
+      src_tab[i] = p.row_map ? p.row_map[src] : src;
+    }
+    __syncthreads();
+  }
   auto load_x = [&](int kt, int r) {
     kt = min(kt, ktiles - 1);
     const int k0 = kt * 32;
@@ -699,9 +712,7 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
       // per thread: its 8 k lie in one segment; past the segments, zeros
       // (read from column 0 of a valid row)
       const int k = k0 + 8 * pch, seg = k / p.din, segc = min(seg, p.nseg - 1);
-      const int shift = (int)(signed char)(p.off_packed >> (8 * segc));
-      int src = clampi(clampi(f0 + prow, 0, p.m - 1) + shift, 0, p.m - 1);
-      if (p.row_map) src = p.row_map[src];
+      const int src = src_tab[segc * BF + prow];
       gvec *xb = (gvec *)(p.xf + (size_t)src * p.ldx + (seg < p.nseg ? k - segc * p.din : 0));
       rx0[r] = xb[0];
       rx1[r] = xb[1];
