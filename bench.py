@@ -184,9 +184,9 @@ def cpu_baseline(conf, n_utts, seconds, threads, min_wall):
 ROOFLINE_KERNEL = "gemm_f32_glds_kernel<catears::Cfg<128, 64, 32, 2, 2>, 2, false>"
 # split-plane hidden layers (split output), the default variants
 SPLIT_ROOFLINE_KERNEL = {
-    # CATEARS_X6_VARIANT 0 = 300; both instantiations (first layer gathered
-    # in the loader, and layers 2-7)
-    "bf16x6": "gemm_bf16x6d_kernel<catears::X6Cfg<256, 128, 4, 2, 2>*",
+    # CATEARS_X6_VARIANT 0 = 300; every instantiation (the first layer
+    # gathered in the loader on 128 x 128 tiles, layers 2-7 on 256 x 128)
+    "bf16x6": "gemm_bf16x6d_kernel<catears::X6Cfg<*",
     "bf16x6_160": "gemm_bf16x6f_kernel<catears::X6Cfg<128, 256, 2, 4, 2>, 8, 0, false>",
     "bf16x6p": "gemm_bf16x6q_kernel<catears::X6Cfg<128, 128, 4, 2, 3>, true, 0>",
     "f16x3": "gemm_f16x3_kernel<catears::X3Cfg<128, 128, 2, 4, 2, 64>, true>",

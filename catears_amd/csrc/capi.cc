@@ -615,6 +615,13 @@ static int ensure_scratch(ce_gpu_ctx *ctx, size_t bytes) {
   return ctx->scratch.alloc(bytes);
 }
 
+// the latency GEMM's slice partials (one window of rows)
+static int ensure_lat_part(ce_gpu_ctx *ctx, size_t floats) {
+  if (ctx->lat_part.bytes >= floats * sizeof(float)) return CE_GPU_OK;
+  CE_HIP(hipStreamSynchronize(ctx->stream));
+  return ctx->lat_part.alloc(floats * sizeof(float));
+}
+
 int fbank_frames_per_block();
 
 static hipEvent_t pool_event(ce_gpu_ctx *ctx) {
@@ -1154,8 +1161,18 @@ static bool x6_first_direct() {
   return v && (x6_variant_env() == 0 || x6_variant_env() == 300);
 }
 
+// CATEARS_LAT_FUSED_FINAL=0 keeps the last layer's split-K reduce as its own
+// launch before the finalize (bit-identical; the default fuses the two)
+static bool lat_fused_final() {
+  static const bool v = [] {
+    const char *e = getenv("CATEARS_LAT_FUSED_FINAL");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
+
 static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, int ldx, int rows,
-                         const int *row_map, const float **y, int *ldy) {
+                         const int *row_map, const float **y, int *ldy, LatTail *tail) {
   int max_in = 0;
   for (const Step &st : m->steps) max_in = std::max(max_in, st.gemm.kpad);
   for (const Step &st : m->steps) max_in = std::max(max_in, (st.gemm.n + 31) / 32 * 32);
@@ -1217,7 +1234,10 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
     {
       ProfScope prof(ctx, CE_GPU_PROF_GEMM);
       if (ctx->latency) {
-        CE_TRY(launch_gemm_bf16x6_lat(ctx->stream, a));
+        const size_t pf = x6_lat_part_floats(a.m, a.n, x6_lat_slices(a.kpad, a.n));
+        CE_TRY(ensure_lat_part(ctx, pf));
+        if (last && lat_fused_final()) a.tail = tail;  // the reduce may run inside the finalize
+        CE_TRY(launch_gemm_bf16x6_lat(ctx->stream, a, ctx->lat_part.as<float>(), pf));
       } else {
         CE_TRY(launch_gemm_bf16x6(ctx->stream, a));
       }
@@ -1454,19 +1474,25 @@ static int run_steps_i8(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, 
 }
 
 static int run_steps(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, int ldx, int rows,
-                     const int *row_map, const uint32_t *row_edge, const float **y, int *ldy) {
+                     const int *row_map, const uint32_t *row_edge, const float **y, int *ldy,
+                     LatTail *tail = nullptr) {
+  if (tail) tail->active = false;
   if (m->int8) return run_steps_i8(ctx, m, x, ldx, rows, row_map, row_edge, y, ldy);
   if (m->gemm == CE_GPU_GEMM_F16X3) return run_steps_x3(ctx, m, x, ldx, rows, row_map, y, ldy);
   if (m->gemm == CE_GPU_GEMM_BF16X6_PLANES) return run_steps_x6(ctx, m, x, ldx, rows, row_map, y, ldy);
   if (m->gemm == CE_GPU_GEMM_BF16X6)
-    return x6_f32in() ? run_steps_x6f(ctx, m, x, ldx, rows, row_map, y, ldy)
+    return x6_f32in() ? run_steps_x6f(ctx, m, x, ldx, rows, row_map, y, ldy, tail)
                       : run_steps_x6(ctx, m, x, ldx, rows, row_map, y, ldy);
   return run_steps_f32(ctx, m, x, ldx, rows, row_map, y, ldy);
 }
 
 // launch_finalize on rows first .. first + rows - 1 of run_steps' output
+// (or of its deferred latency tail: the last layer's reduce in the same
+// launch)
 static int finalize_output(ce_gpu_ctx *ctx, const float *y, int ldy, int first, int rows, int dim,
-                           bool log_softmax, const float *log_prior, const int *row_dst, float *out) {
+                           bool log_softmax, const float *log_prior, const int *row_dst, float *out,
+                           const LatTail &tail = LatTail()) {
+  if (tail.active) return launch_lat_finalize(ctx->stream, tail, first, rows, log_softmax, log_prior, row_dst, out);
   return launch_finalize(ctx->stream, y + (size_t)first * ldy, ldy, rows, dim, log_softmax, log_prior, row_dst,
                          out);
 }
@@ -1547,10 +1573,11 @@ int ce_gpu_am_forward(ce_gpu_ctx *ctx, const ce_gpu_model *m, const ce_gpu_plan 
     const float *y = nullptr;
     int ldy = 0;
     const uint32_t *row_edge = p->d_row_edge.as<uint32_t>() + c.map_base;
-    CE_TRY(run_steps(ctx, m, d_feats, m->input_dim, c.rows, row_src, row_edge, &y, &ldy));
+    LatTail tail;
+    CE_TRY(run_steps(ctx, m, d_feats, m->input_dim, c.rows, row_src, row_edge, &y, &ldy, &tail));
     ProfScope prof(ctx, CE_GPU_PROF_FINALIZE);
     CE_TRY(finalize_output(ctx, y, ldy, 0, c.rows, m->num_pdfs, m->final_log_softmax, m->log_prior.as<float>(),
-                           row_dst, d_loglik));
+                           row_dst, d_loglik, tail));
   }
   return CE_GPU_OK;
 }
@@ -1596,10 +1623,11 @@ int ce_gpu_nnet_propagate(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *d
   }
   const float *y = nullptr;
   int ldy = 0;
-  CE_TRY(run_steps(ctx, m, d_in, ld_in, rows, nullptr, nullptr, &y, &ldy));
+  LatTail tail;
+  CE_TRY(run_steps(ctx, m, d_in, ld_in, rows, nullptr, nullptr, &y, &ldy, &tail));
   ProfScope prof(ctx, CE_GPU_PROF_FINALIZE);
   return finalize_output(ctx, y, ldy, m->net_left, out_rows, m->num_pdfs, m->final_log_softmax,
-                         subtract_prior ? m->log_prior.as<float>() : nullptr, nullptr, d_out);
+                         subtract_prior ? m->log_prior.as<float>() : nullptr, nullptr, d_out, tail);
 }
 
 int ce_gpu_nnet_propagate_blocks(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *d_in, int ld_in,
@@ -1653,10 +1681,11 @@ int ce_gpu_nnet_propagate_blocks(ce_gpu_ctx *ctx, const ce_gpu_model *m, const f
   int ldy = 0;
   // blocks are independent: the rows a Splice reads across a block boundary
   // only feed rows that block's Narrow drops
-  CE_TRY(run_steps(ctx, m, d_in, ld_in, rows, nullptr, d_edge, &y, &ldy));
+  LatTail tail;
+  CE_TRY(run_steps(ctx, m, d_in, ld_in, rows, nullptr, d_edge, &y, &ldy, &tail));
   ProfScope prof(ctx, CE_GPU_PROF_FINALIZE);
   return finalize_output(ctx, y, ldy, 0, rows, m->num_pdfs, m->final_log_softmax,
-                         subtract_prior ? m->log_prior.as<float>() : nullptr, d_dst, d_out);
+                         subtract_prior ? m->log_prior.as<float>() : nullptr, d_dst, d_out, tail);
 }
 
 static int score_feats(ce_gpu_ctx *ctx, const ce_gpu_model *m, const ce_gpu_plan *p, const float *d_global_stats,

@@ -154,6 +154,24 @@ __device__ __forceinline__ float apply_post(float y, float sc, float of, const i
   return y;
 }
 
+// The latency GEMM's split-K reduce (kernels/gemm_bf16x6_lat.hip): the S
+// slice partials of 4 consecutive outputs (slice s at src + s * stride) summed
+// in slice order, 16 loads in flight at a time.
+__device__ __forceinline__ float4 lat_slice_sum(const float *src, size_t stride, int slices) {
+  float4 sum = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  for (int s0 = 0; s0 < slices; s0 += 16) {
+    float4 v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (s0 + u < slices) v[u] = *reinterpret_cast<const float4 *>(src + (size_t)(s0 + u) * stride);
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (s0 + u < slices)
+        sum = s0 + u == 0 ? v[u] : make_float4(sum.x + v[u].x, sum.y + v[u].y, sum.z + v[u].z, sum.w + v[u].w);
+  }
+  return sum;
+}
+
 // Calls f(std::integral_constant<int, MODE>) for the runtime mode.
 template <class F>
 __device__ __forceinline__ void with_post_mode(int mode, F &&f) {
@@ -265,6 +283,21 @@ struct X6Gemm {
   float *y32 = nullptr;
   uint16_t *y16 = nullptr;
   int ldy = 0, py = 0;
+  // latency kernel: leave the last layer's slice reduce to
+  // launch_lat_finalize (described in *tail) when it can run there
+  struct LatTail *tail = nullptr;
+};
+
+// The last layer's slice partials when its reduce runs inside the finalize
+// (latency mode): out(f, c) = post(((p0 + p1) + ..) + bias), rows f of
+// part[s * m + f][n].
+struct LatTail {
+  bool active = false;
+  const float *part = nullptr;
+  int slices = 0, m = 0, n = 0;
+  const float *bias = nullptr, *bn_scale = nullptr, *bn_offset = nullptr;
+  int post[4] = {0, 0, 0, 0};
+  int npost = 0;
 };
 
 }  // namespace catears
@@ -281,6 +314,7 @@ struct ce_gpu_ctx {
   catears::DevBuf scratch;     // reductions / int8 operand staging (grown on demand)
   catears::DevBuf blk_maps;    // ce_gpu_nnet_propagate_blocks: row_dst + row_edge
   catears::DevBuf overflow;    // int: an f16x3 split left the fp16 range (ce_gpu_ctx_overflow)
+  catears::DevBuf lat_part;    // latency GEMM: slice partials (grown on demand)
   int latency = 0;             // ce_gpu_ctx_set_latency: split-K GEMMs for small batches
   int fbank_mode = 0;          // ce_gpu_ctx_set_fbank: CE_GPU_FBANK_EXACT / _FAST
   std::vector<int32_t> h_blk_maps;
@@ -409,7 +443,24 @@ constexpr int kX6DirUnits = 256;  // gemm_bf16x6d_kernel's unit tile
 // tiles, K split over a block's four waves (a function of K only) and summed
 // in wave order in LDS, + bias / ReLU / BatchNorm; needs the weight fragment
 // image (a.wd) and fp32 activations (din a multiple of 8).
-int launch_gemm_bf16x6_lat(hipStream_t s, const X6Gemm &a);
+// Latency mode (kernels/gemm_bf16x6_lat.hip): K split into
+// x6_lat_slices(kpad, n) slices (a function of K and N only), every slice's
+// fp32 partial stored, then summed in slice order by a reduce kernel that
+// applies bias / ReLU / BatchNorm; needs the weight fragment image (a.wd) and
+// fp32 activations (din a multiple of 8: a segment may end inside a K-tile).
+// part: x6_lat_part_floats(rows, n, slices) floats.  With a.tail set and the
+// rows within one window (rows <= kX6LatWindow, n % 4 == 0, n <= 4096) the
+// reduce is left to launch_lat_finalize (a.tail->active).
+constexpr int kX6LatWindow = 1024;
+int x6_lat_slices(int kpad, int n);
+size_t x6_lat_part_floats(int rows, int n, int slices);
+int launch_gemm_bf16x6_lat(hipStream_t s, const X6Gemm &a, float *part, size_t part_floats);
+// The last layer's slice reduce fused with the finalize: rows first ..
+// first + rows - 1 of a deferred tail summed, + bias, post chain, then
+// (log-softmax) - prior into out (row_dst as launch_finalize) -- the bits of
+// the reduce launch followed by launch_finalize.
+int launch_lat_finalize(hipStream_t s, const LatTail &t, int first, int rows, bool log_softmax,
+                        const float *log_prior, const int *row_dst, float *out);
 // splice_pad (below) written as three bf16 planes of width po: out row r at
 // out + r * 3 * po.
 int launch_splice_pad_split(hipStream_t s, const float *in, int ld_in, int rows, int din, int nseg, const int *off,

@@ -1131,7 +1131,7 @@ int launch_d(hipStream_t s, X6Args p) {
   p.tiles_n = (p.n + C::BW - 1) / C::BW;
   p.tiles_m = (p.m + C::BF - 1) / C::BF;
   dim3 grid(p.tiles_m * p.tiles_n), block(C::NT);
-  if (p.row_map || p.nseg > 1 && p.din % 32 != 0)
+  if (p.row_map || (p.nseg > 1 && p.din % 32 != 0))
     hipLaunchKernelGGL((gemm_bf16x6d_kernel<C, true>), grid, block, 0, s, p);
   else
     hipLaunchKernelGGL((gemm_bf16x6d_kernel<C>), grid, block, 0, s, p);
@@ -1163,6 +1163,18 @@ int x6_variant() {
   static int v = [] {
     const char *e = getenv("CATEARS_X6_VARIANT");
     return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+// CATEARS_X6_FIRST_TILE: unit width of the gathered first layer's tiles.
+// 128 (default): 256 blocks for a 4072-row batch instead of 128, 26.5 ->
+// 20.9 us per launch in a serial run (r4c); 256: the hidden layers' tiles.
+// Same bits either way (tests/test_gpu_x6_variants.py).
+int x6_first_tile() {
+  static int v = [] {
+    const char *e = getenv("CATEARS_X6_FIRST_TILE");
+    return e ? atoi(e) : 128;
   }();
   return v;
 }
@@ -1247,6 +1259,9 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
         if (a.wd) {
           if (a.wd_kt * 32 < a.kpad || (reinterpret_cast<uintptr_t>(a.wd) & 15))
             return fail(CE_GPU_EINVAL, "gemm_bf16x6: weight fragment image does not cover K");
+          // the gathered first layer (K of a few tiles: prologue and
+          // epilogue bound) on 128 x 128 tiles -- twice the blocks
+          if (first && x6_first_tile() == 128) return launch_d<X6Cfg<128, 128, 2, 4, 2>>(s, p);
           return launch_d<X6Cfg<kX6DirUnits, 128, 4, 2, 2>>(s, p);
         }
         [[fallthrough]];

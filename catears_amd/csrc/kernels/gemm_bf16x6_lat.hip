@@ -1,34 +1,35 @@
 // gemm_bf16x6_lat.hip -- latency mode of the TDNN GEMMs (ce_gpu_ctx_set_latency):
 // the streaming AcousticModel chunk (src/am.cc:115-142: chunk_size + L + R
 // rows, 70 for TDNN-S) or one utterance per call, where a row block is far
-// too small to fill the chip with the throughput kernel's 256 x 128 tiles.
+// too small to fill the chip with output tiles.
 //
 // Same contraction and products as gemm_bf16x6d_kernel (Splice + Narrow +
 // LinearLayer + bias / ReLU / BatchNorm, src/nnet.cc:22-43,50-75,106-160;
 // bf16x6: w0x0, w0x1, w1x0, w1x1, w0x2, w2x0 per K-tile, fp32 accumulate),
-// as ONE launch per layer with no partial buffer in memory:
+// with K split into S slices so a 70-row block still spreads over ~256 CUs:
 //
-//   block = 16 units x 16 TF rows, kL2Waves waves.  Wave w takes the K-tiles
-//   [w per, (w + 1) per) (per = ceil(K-tiles / kL2Waves): a function of K
-//   only).  Both operands go straight to registers: the weights from the
-//   MFMA-fragment image (X6Gemm::wd, one global_load_dwordx4 per lane and
-//   plane), the activations as the lane's 8 consecutive floats of one row
-//   (two 16-byte loads, through the splice offsets and, for the first layer,
-//   the caller's row_map), split into the three bf16 planes in registers --
-//   the B-fragment layout of v_mfma_f32_16x16x32_bf16 is one row's 8
-//   consecutive k per lane, so no LDS transpose is needed.  The next K-tile's
-//   loads are in flight during this one's MFMAs.  At the end the four waves'
-//   fp32 partial tiles meet in LDS and are summed in wave order
-//   (((p0 + p1) + p2) + p3), + bias, ReLU / BatchNorm in the reference's
-//   rounding order, stored.
+//   lat_gemm_kernel    block (row tile, 64-unit column tile, slice s): every
+//                      weight fragment of its <= 6 K-tiles is loaded at once,
+//                      straight from the MFMA-fragment image into registers
+//                      (X6Gemm::wd: the loads of the whole slice are in flight
+//                      together -- a small block's K loop is latency bound
+//                      otherwise), the activation tiles are split into bf16
+//                      planes in LDS, and the slice's fp32 partial tile is
+//                      stored to part[s][row][unit];
+//   lat_reduce_kernel  sums the S partials of each output element in slice
+//                      order, adds the bias and applies ReLU / BatchNorm in the
+//                      reference's rounding order.
 //
-// Small row blocks get many blocks from the 16-unit tiles (70 rows of a
-// 1024-unit layer: 64 x 5 = 320 blocks), so no K split across blocks -- and
-// no reduce launch -- is needed to spread a chunk over the chip.  The sum
-// order depends on K only, never on the row count or the tile shape (TF), so
-// a row's result does not depend on the block it is scored in
-// (AcousticModel's batching contract).
+// The kernel boundary orders the partials for the reduction: no inter-block
+// hand-off, no tickets, no fences.  S depends on K and N only
+// (x6_lat_slices), never on the row count, so a row's result does not depend
+// on the block it is scored in (AcousticModel batching contract).
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <string>
+#include <type_traits>
 
 #include "../internal.h"
 
@@ -39,21 +40,22 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kL2Waves = 4;  // K split among a block's waves (part of the summation order)
+constexpr int kLatNW = 4;              // waves per block, 16 units each
+constexpr int kLatBW = 16 * kLatNW;    // units per block
+constexpr int kLatMaxKt = 8;           // K-tiles (of 32) per slice: all its weights in registers
+constexpr int kLatTarget = 256;        // blocks per row tile the slice rule aims at
 
-struct Lat2Args {
+struct LatArgs {
   const float *xf;
   const uint16_t *wd;
+  float *part;
   const int *row_map;
   int ldx, wd_kt;
   int m, n, kpad, din, nseg;
   uint64_t off_packed;
-  int per, tiles_n;
-  const float *bias, *bn_scale, *bn_offset;
-  int post[4];
-  int npost;
-  float *y;
-  int ldy;
+  int slices, per;  // S, K-tiles per slice
+  int tiles_n, row0, rows;  // this window: rows row0 .. row0 + rows - 1
+  int row_tiles, rtb;       // row tiles in the window, row tiles per block
 };
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
@@ -76,145 +78,335 @@ __device__ __forceinline__ Planes2 split3_pair(float a, float b) {
   return Planes2{p0, p1, cvt(sa, sb)};
 }
 
-// One K-tile's operands of a wave, in registers.
-template <int TF>
-struct Tile {
-  bf16x8 w[3];
-  f32x4 x[TF][2];
-};
+// MULTI: the block loops over several row tiles (large windows); a single
+// tile is straight-line code (a loop would make the compiler drain the weight
+// loads before the activation loads are issued, at the loop header).
+// KT: K-tiles per slice the block is sized for (>= the slice's per).
+template <int TF, int KT, bool MULTI, int DIAG = 0>
+__global__ __launch_bounds__(64 * kLatNW, MULTI && TF == 4 && KT <= 6 ? 2 : 1) void lat_gemm_kernel(LatArgs p) {
+#ifndef CATEARS_DIAG
+  static_assert(DIAG == 0, "diagnostic schedules are CATEARS_DIAG builds only");
+#endif
+  constexpr int BF = 16 * TF;
+  constexpr int KSTAGE = 3 * BF * 64;  // bytes: the planes of one K-tile
+  __shared__ __attribute__((aligned(1024))) char smem[KT * KSTAGE];
+  typedef const __attribute__((address_space(1))) bf16x8 gfrag;
+  typedef const __attribute__((address_space(1))) f32x4 gvec;
+  auto swz = [](int row) { return ((row >> 3) & 1) << 1; };
 
-template <int TF>
-__device__ __forceinline__ void load_tile(const Lat2Args &p, int kt, int f0, int lane,
-                                          const __attribute__((address_space(1))) bf16x8 *wb, Tile<TF> &t) {
-#pragma unroll
-  for (int pl = 0; pl < 3; ++pl) t.w[pl] = wb[(kt * 3 + pl) * 64];
-  // this lane's 8 k of the K-tile lie in one segment (din % 8 == 0); k past
-  // the segments is K's zero padding: column 0 of a valid row is read and the
-  // value replaced by zeros (the address stays inside the row)
-  const int k = kt * 32 + 8 * (lane >> 4);
-  const int seg = k / p.din, segc = min(seg, p.nseg - 1);
-  const int shift = (int)(signed char)(p.off_packed >> (8 * segc));
-  const int col = seg < p.nseg ? k - segc * p.din : 0;
-#pragma unroll
-  for (int j = 0; j < TF; ++j) {
-    int row = clampi(clampi(f0 + 16 * j + (lane & 15), 0, p.m - 1) + shift, 0, p.m - 1);
-    if (p.row_map) row = p.row_map[row];
-    const f32x4 *src = reinterpret_cast<const f32x4 *>(p.xf + (size_t)row * p.ldx + col);
-    t.x[j][0] = src[0];
-    t.x[j][1] = src[1];
-  }
-  if (seg >= p.nseg) {
-#pragma unroll
-    for (int j = 0; j < TF; ++j) t.x[j][0] = t.x[j][1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  }
-}
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int s = blockIdx.x % p.slices, t = blockIdx.x / p.slices;
+  const int ct = t % p.tiles_n, rg = t / p.tiles_n;
+  const int n0 = ct * kLatBW;
+  const int ktiles = p.kpad / 32, kt0 = s * p.per, nk = min(p.per, ktiles - kt0);
 
-// the six products of one K-tile, per element in the order of every bf16x6
-// kernel: a0b0, a0b1, a1b0, a1b1, a0b2, a2b0
-template <int TF>
-__device__ __forceinline__ void mma_tile(const Tile<TF> &t, f32x4 (&acc)[TF]) {
-  bf16x8 b0[TF], b1[TF], b2[TF];
+  // the activation rows of the slice: task q = (K-tile i, row, 8-float
+  // chunk) spread evenly over the block's threads.  Every address first (the
+  // row_map gather ahead of the weight loads: vector loads retire in order, so
+  // a wait on it would otherwise wait on the weights too), then every load
+  // (branch-free, so all of a thread's loads are in flight together), then the
+  // splits and LDS stores.  A chunk's 8 k lie in one segment (din % 8 == 0);
+  // k past the segments is K's zero padding; tasks past the slice load a
+  // clamped (valid) address.
+  constexpr int NT = 64 * kLatNW, TASKS = KT * BF * 4, TPT = (TASKS + NT - 1) / NT;
+  gvec *xptr[TPT];
+  bool xlive[TPT];
+  auto act_addr = [&](int rt) {
+    const int f0 = p.row0 + rt * BF;
+    int xrow[TPT], xcol[TPT];
 #pragma unroll
-  for (int j = 0; j < TF; ++j) {
-    const f32x4 v0 = t.x[j][0], v1 = t.x[j][1];
+    for (int j = 0; j < TPT; ++j) {
+      const int q = min(tid + j * NT, TASKS - 1);
+      const int i = q / (BF * 4), prow = (q >> 2) % BF, pch = q & 3;
+      const int k = min(kt0 + i, ktiles - 1) * 32 + 8 * pch;
+      const int seg = k / p.din, segc = min(seg, p.nseg - 1);
+      const int shift = (int)(signed char)(p.off_packed >> (8 * segc));
+      xrow[j] = clampi(clampi(f0 + prow, 0, p.m - 1) + shift, 0, p.m - 1);
+      xcol[j] = k - segc * p.din;
+      xlive[j] = tid + j * NT < TASKS && i < nk && seg < p.nseg && !(DIAG & 2);
+    }
+    if (p.row_map) {
+#pragma unroll
+      for (int j = 0; j < TPT; ++j) xrow[j] = p.row_map[xrow[j]];
+    }
+#pragma unroll
+    for (int j = 0; j < TPT; ++j) xptr[j] = (gvec *)(p.xf + (size_t)xrow[j] * p.ldx + xcol[j]);
+  };
+  act_addr(rg * p.rtb);
+  __builtin_amdgcn_sched_barrier(0);
+
+  // 1. every weight fragment of the slice, at once (units n0 + 16 wave ..)
+  bf16x8 wa[KT][3];
+  {
+    gfrag *wb = (gfrag *)(p.wd + ((size_t)((n0 >> 4) + wave) * p.wd_kt * 3 * 64 + lane) * 8);
+    // branch-free: K-tiles past the slice load the last one (never used)
+#pragma unroll
+    for (int i = 0; i < KT; ++i)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+        wa[i][pl] = wb[(min(kt0 + i, ktiles - 1) * 3 + pl) * 64];
+        if (DIAG & 1) wa[i][pl] = bf16x8{};
+      }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+
+  // the block's row tiles, one after another with the weights kept in
+  // registers (a window of many row tiles reads each weight once per block)
+  const int rt_end = min(p.row_tiles, (rg + 1) * p.rtb);
+  const int foff = (lane & 15) * 64 + (((lane >> 4) ^ (((lane >> 3) & 1) << 1)) * 16);
+  const int n = n0 + wave * 16 + 4 * (lane >> 4);
+  for (int rt = rg * p.rtb; rt < rt_end; ++rt) {
+  const int f0 = p.row0 + rt * BF;
+  if (rt > rg * p.rtb) {
+    __syncthreads();  // the previous tile's LDS reads are done
+    act_addr(rt);
+  }
+
+  // 2. the activation rows (addresses computed above), split into planes
+  f32x4 xv[TPT][2];
+#pragma unroll
+  for (int j = 0; j < TPT; ++j) {
+    xv[j][0] = xptr[j][0];
+    xv[j][1] = xptr[j][1];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int j = 0; j < TPT; ++j) {
+    const int q = tid + j * NT;
+    const int i = q / (BF * 4), prow = (q >> 2) % BF, pch = q & 3;
+    if (q >= TASKS || i >= nk) continue;
+    const f32x4 zero = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    const f32x4 v0 = xlive[j] ? xv[j][0] : zero, v1 = xlive[j] ? xv[j][1] : zero;
     const Planes2 q0 = split3_pair(v0.x, v0.y), q1 = split3_pair(v0.z, v0.w);
     const Planes2 q2 = split3_pair(v1.x, v1.y), q3 = split3_pair(v1.z, v1.w);
-    b0[j] = __builtin_bit_cast(bf16x8, u32x4{q0.h, q1.h, q2.h, q3.h});
-    b1[j] = __builtin_bit_cast(bf16x8, u32x4{q0.m, q1.m, q2.m, q3.m});
-    b2[j] = __builtin_bit_cast(bf16x8, u32x4{q0.l, q1.l, q2.l, q3.l});
+    char *st = smem + i * KSTAGE;
+    const int off = prow * 64 + ((pch ^ swz(prow)) * 16);
+    *reinterpret_cast<u32x4 *>(st + off) = u32x4{q0.h, q1.h, q2.h, q3.h};
+    *reinterpret_cast<u32x4 *>(st + BF * 64 + off) = u32x4{q0.m, q1.m, q2.m, q3.m};
+    *reinterpret_cast<u32x4 *>(st + 2 * BF * 64 + off) = u32x4{q0.l, q1.l, q2.l, q3.l};
   }
-#pragma unroll
-  for (int j = 0; j < TF; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(t.w[0], b0[j], acc[j], 0, 0, 0);
-#pragma unroll
-  for (int j = 0; j < TF; ++j) {
-    acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(t.w[0], b1[j], acc[j], 0, 0, 0);
-    acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(t.w[1], b0[j], acc[j], 0, 0, 0);
-    acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(t.w[1], b1[j], acc[j], 0, 0, 0);
-  }
-#pragma unroll
-  for (int j = 0; j < TF; ++j) {
-    acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(t.w[0], b2[j], acc[j], 0, 0, 0);
-    acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(t.w[2], b0[j], acc[j], 0, 0, 0);
-  }
-}
+  __syncthreads();
 
-template <int TF, int MODE>
-__global__ __launch_bounds__(64 * kL2Waves) void lat2_kernel(Lat2Args p) {
-  __shared__ f32x4 red[kL2Waves][TF][64];
-  typedef const __attribute__((address_space(1))) bf16x8 gfrag;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int ct = blockIdx.x % p.tiles_n, rt = blockIdx.x / p.tiles_n;
-  const int f0 = rt * 16 * TF;
-  const int ktiles = p.kpad / 32, kt0 = wave * p.per, kt1 = min(kt0 + p.per, ktiles);
-  gfrag *wb = (gfrag *)(p.wd + ((size_t)ct * p.wd_kt * 3 * 64 + lane) * 8);
-
+  // 3. the slice's K-tiles in order, six products per tile in the order of
+  //    every other bf16x6 kernel (per element: a0b0, a0b1, a1b0, a1b1, a0b2,
+  //    a2b0)
   f32x4 acc[TF];
 #pragma unroll
   for (int j = 0; j < TF; ++j) acc[j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  if (kt0 < kt1) {
-    Tile<TF> cur, nxt;
-    load_tile<TF>(p, kt0, f0, lane, wb, cur);
-    int kt = kt0;
-    for (; kt + 1 < kt1; kt += 2) {
-      load_tile<TF>(p, kt + 1, f0, lane, wb, nxt);
-      mma_tile<TF>(cur, acc);
-      if (kt + 2 < kt1) load_tile<TF>(p, kt + 2, f0, lane, wb, cur);
-      mma_tile<TF>(nxt, acc);
+#pragma unroll
+  for (int i = 0; i < KT; ++i) {
+    if (i >= nk) break;
+    const char *st = smem + i * KSTAGE;
+    const bf16x8 (&w)[3] = wa[i];
+    bf16x8 b0[TF], b1[TF];
+#pragma unroll
+    for (int j = 0; j < TF; ++j) b0[j] = *reinterpret_cast<const bf16x8 *>(st + (j * 16) * 64 + foff);
+#pragma unroll
+    for (int j = 0; j < TF; ++j) b1[j] = *reinterpret_cast<const bf16x8 *>(st + (BF + j * 16) * 64 + foff);
+    if constexpr ((DIAG & 4) != 0) {  // keep the operands live without the MFMAs
+      const u32x4 a = __builtin_bit_cast(u32x4, w[0]) ^ __builtin_bit_cast(u32x4, w[1]) ^
+                      __builtin_bit_cast(u32x4, w[2]) ^ __builtin_bit_cast(u32x4, b0[0]) ^
+                      __builtin_bit_cast(u32x4, b1[TF - 1]);
+      acc[0].x += __builtin_bit_cast(float, a.x ^ a.y ^ a.z ^ a.w);
+      continue;
     }
-    if (kt < kt1) mma_tile<TF>(cur, acc);
+#pragma unroll
+    for (int j = 0; j < TF; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], b0[j], acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < TF; ++j) {
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], b1[j], acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1], b0[j], acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1], b1[j], acc[j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < TF; ++j) {
+      const bf16x8 b2 = *reinterpret_cast<const bf16x8 *>(st + (2 * BF + j * 16) * 64 + foff);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], b2, acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[2], b0[j], acc[j], 0, 0, 0);
+    }
   }
 
-  // the waves' partial tiles, summed in wave order; lane holds units
-  // n .. n+3 of frame f of each fragment
+  // 4. the partial tile: lane holds units n .. n+3 of frame f per fragment
+  if (n < p.n && !(DIAG & 8)) {
 #pragma unroll
-  for (int j = 0; j < TF; ++j) red[wave][j][lane] = acc[j];
-  __syncthreads();
-  const int n = ct * 16 + 4 * (lane >> 4);
-  if (n >= p.n) return;
-  const f32x4 bias = p.bias ? *reinterpret_cast<const f32x4 *>(p.bias + n) : f32x4{-0.0f, -0.0f, -0.0f, -0.0f};
-  const f32x4 sc = p.bn_scale ? *reinterpret_cast<const f32x4 *>(p.bn_scale + n) : f32x4{1.0f, 1.0f, 1.0f, 1.0f};
-  const f32x4 of = p.bn_offset ? *reinterpret_cast<const f32x4 *>(p.bn_offset + n) : f32x4{-0.0f, -0.0f, -0.0f, -0.0f};
-  for (int j = wave; j < TF; j += kL2Waves) {
-    const int f = f0 + 16 * j + (lane & 15);
-    if (f >= p.m) continue;
-    f32x4 s = red[0][j][lane];
+    for (int j = 0; j < TF; ++j) {
+      const int f = f0 + j * 16 + (lane & 15);
+      if (f >= p.row0 + p.rows || f >= p.m) continue;
+      *reinterpret_cast<f32x4 *>(p.part + ((size_t)s * p.rows + (f - p.row0)) * p.n + n) = acc[j];
+    }
+  }
+  if constexpr (!MULTI) break;
+  }  // row tiles
+}
+
+// The last layer's reduce fused into the finalize (LogSoftmax + log prior +
+// row scatter): one 256-thread block per row, thread t holding float4 chunks
+// t, t + 256, .. (rowops.hip finalize_vec_kernel's layout and order); each
+// chunk summed over the slices exactly as lat_reduce_kernel does (+ bias,
+// post chain), then the finalize's arithmetic in its order.
+template <bool LOGSM, int MODE>
+__global__ __launch_bounds__(256) void lat_finalize_kernel(LatTail t, int first, const float *prior,
+                                                           const int *row_dst, float *out) {
+  constexpr int kPer = 4;
+  __shared__ float wsum[4];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const int dst = row_dst ? row_dst[row] : row;
+  if (dst < 0) return;  // block-uniform
+  const int d4 = t.n >> 2;
+  const float *src = t.part + (size_t)(first + row) * t.n;
+  const size_t stride = (size_t)t.m * t.n;
+  f32x4 v[kPer];
 #pragma unroll
-    for (int w = 1; w < kL2Waves; ++w) s += red[w][j][lane];
-    f32x4 v;
+  for (int j = 0; j < kPer; ++j) {
+    const int c = min(tid + 256 * j, d4 - 1);  // clamped: used only when in range
+    const float4 s4 = lat_slice_sum(src + 4 * c, stride, t.slices);
+    const f32x4 bias = t.bias ? reinterpret_cast<const f32x4 *>(t.bias)[c] : f32x4{-0.0f, -0.0f, -0.0f, -0.0f};
+    const f32x4 sc = t.bn_scale ? reinterpret_cast<const f32x4 *>(t.bn_scale)[c] : f32x4{1.0f, 1.0f, 1.0f, 1.0f};
+    const f32x4 of = t.bn_offset ? reinterpret_cast<const f32x4 *>(t.bn_offset)[c] : f32x4{-0.0f, -0.0f, -0.0f, -0.0f};
+    const f32x4 sum = f32x4{s4.x, s4.y, s4.z, s4.w};
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = apply_post<MODE>(s[e] + bias[e], sc[e], of[e], p.post, p.npost);
-    *reinterpret_cast<f32x4 *>(p.y + (int64_t)f * p.ldy + n) = v;
+    for (int e = 0; e < 4; ++e) v[j][e] = apply_post<MODE>(sum[e] + bias[e], sc[e], of[e], t.post, t.npost);
+  }
+  float s = 0.0f;
+  if (LOGSM) {
+#pragma unroll
+    for (int j = 0; j < kPer; ++j)
+      if (tid + 256 * j < d4) s += expf(v[j].x) + expf(v[j].y) + expf(v[j].z) + expf(v[j].w);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
+    if ((tid & 63) == 0) wsum[tid >> 6] = s;
+    __syncthreads();
+    s = ((wsum[0] + wsum[1]) + wsum[2]) + wsum[3];
+  }
+  const float ls = LOGSM ? logf(s) : 0.0f;
+  f32x4 *o = reinterpret_cast<f32x4 *>(out + (int64_t)dst * t.n);
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int c = tid + 256 * j;
+    if (c < d4) {
+      f32x4 y = v[j];
+      if (LOGSM) y = y - ls;
+      if (prior) y = y - reinterpret_cast<const f32x4 *>(prior)[c];
+      o[c] = y;
+    }
   }
 }
 
-template <int TF>
-void launch_lat2(hipStream_t s, const Lat2Args &p, int mode) {
-  const int64_t blocks = (int64_t)p.tiles_n * ((p.m + 16 * TF - 1) / (16 * TF));
-  const dim3 grid((unsigned)blocks), block(64 * kL2Waves);
-  switch (mode) {
-    case kPostModeNone: hipLaunchKernelGGL((lat2_kernel<TF, kPostModeNone>), grid, block, 0, s, p); break;
-    case kPostModeRelu: hipLaunchKernelGGL((lat2_kernel<TF, kPostModeRelu>), grid, block, 0, s, p); break;
-    case kPostModeBn: hipLaunchKernelGGL((lat2_kernel<TF, kPostModeBn>), grid, block, 0, s, p); break;
-    case kPostModeReluBn: hipLaunchKernelGGL((lat2_kernel<TF, kPostModeReluBn>), grid, block, 0, s, p); break;
-    case kPostModeBnRelu: hipLaunchKernelGGL((lat2_kernel<TF, kPostModeBnRelu>), grid, block, 0, s, p); break;
-    default: hipLaunchKernelGGL((lat2_kernel<TF, kPostModeGeneric>), grid, block, 0, s, p); break;
+struct LatReduceArgs {
+  const float *part;
+  const float *bias, *bn_scale, *bn_offset;
+  float *y;
+  int slices, rows, n, row0, ldy;
+  int post[4];
+  int npost, post_mode;
+};
+
+// One thread per 4 consecutive units of one row: the slices' partials summed
+// in slice order (the same value whatever row block the row was scored in),
+// then + bias and the post chain (the GEMM epilogues' order and roundings).
+template <int MODE>
+__global__ __launch_bounds__(64) void lat_reduce_kernel(LatReduceArgs p) {
+  const int n4 = p.n >> 2;
+  const int64_t idx = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (idx >= (int64_t)p.rows * n4) return;
+  const int r = (int)(idx / n4), n = (int)(idx - (int64_t)r * n4) * 4;
+  const size_t stride = (size_t)p.rows * p.n;
+  const float *src = p.part + (size_t)r * p.n + n;
+  const float4 s4 = lat_slice_sum(src, stride, p.slices);
+  const f32x4 sum = f32x4{s4.x, s4.y, s4.z, s4.w};
+  const f32x4 bias = p.bias ? *reinterpret_cast<const f32x4 *>(p.bias + n) : f32x4{-0.0f, -0.0f, -0.0f, -0.0f};
+  const f32x4 sc = p.bn_scale ? *reinterpret_cast<const f32x4 *>(p.bn_scale + n) : f32x4{1.0f, 1.0f, 1.0f, 1.0f};
+  const f32x4 of = p.bn_offset ? *reinterpret_cast<const f32x4 *>(p.bn_offset + n) : f32x4{-0.0f, -0.0f, -0.0f, -0.0f};
+  f32x4 v;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = apply_post<MODE>(sum[e] + bias[e], sc[e], of[e], p.post, p.npost);
+  *reinterpret_cast<f32x4 *>(p.y + (int64_t)(p.row0 + r) * p.ldy + n) = v;
+}
+
+// Row tiles per block: enough blocks for two per CU (the many-tile kernel's
+// occupancy), the rest looped with the weights kept in registers rather than
+// re-read per tile.  The partition changes which block computes a tile, never
+// the tile's sums.
+int lat_rtb(int row_tiles, int blocks_per_tile) {
+  static const int env = [] {
+    const char *e = getenv("CATEARS_LAT_RTB");
+    return e ? atoi(e) : 0;
+  }();
+  const int rtb = env > 0 ? env : row_tiles * blocks_per_tile / (2 * kLatTarget);
+  return std::max(1, std::min(rtb, row_tiles));
+}
+
+template <int TF, int KT>
+void launch_lat_gemm_kt(hipStream_t s, const LatArgs &p, dim3 grid, dim3 block) {
+#ifdef CATEARS_DIAG
+  static const int diag = [] {
+    const char *e = getenv("CATEARS_LAT_DIAG");
+    return e ? atoi(e) : 0;
+  }();
+  switch (diag) {
+    case 0: break;
+#define CE_LAT_DIAG(D) \
+  case D: hipLaunchKernelGGL((lat_gemm_kernel<TF, KT, true, D>), grid, block, 0, s, p); return;
+    CE_LAT_DIAG(1) CE_LAT_DIAG(2) CE_LAT_DIAG(3) CE_LAT_DIAG(4) CE_LAT_DIAG(8) CE_LAT_DIAG(12) CE_LAT_DIAG(15)
+#undef CE_LAT_DIAG
+    default: break;
   }
+#endif
+  if (p.rtb > 1)
+    hipLaunchKernelGGL((lat_gemm_kernel<TF, KT, true>), grid, block, 0, s, p);
+  else
+    hipLaunchKernelGGL((lat_gemm_kernel<TF, KT, false>), grid, block, 0, s, p);
+}
+
+template <int TF>
+void launch_lat_gemm(hipStream_t s, LatArgs p) {
+  p.row_tiles = (p.rows + 16 * TF - 1) / (16 * TF);
+  p.rtb = lat_rtb(p.row_tiles, p.tiles_n * p.slices);
+  const int groups = (p.row_tiles + p.rtb - 1) / p.rtb;
+  const dim3 grid(groups * p.tiles_n * p.slices), block(64 * kLatNW);
+  // the block sized for the slice (its weights all in registers)
+  if (p.per <= 2)
+    launch_lat_gemm_kt<TF, 2>(s, p, grid, block);
+  else if (p.per <= 4)
+    launch_lat_gemm_kt<TF, 4>(s, p, grid, block);
+  else if (p.per <= 6)
+    launch_lat_gemm_kt<TF, 6>(s, p, grid, block);
+  else
+    launch_lat_gemm_kt<TF, 8>(s, p, grid, block);
 }
 
 }  // namespace
 
-int launch_gemm_bf16x6_lat(hipStream_t s, const X6Gemm &a) {
+int x6_lat_slices(int kpad, int n) {
+  const int ktiles = kpad / 32, cols = (n + kLatBW - 1) / kLatBW;
+  // at most kLatTarget blocks per row tile (one wave of blocks over the CUs)
+  int slices = std::max(1, std::min(ktiles, kLatTarget / cols));
+  int per = (ktiles + slices - 1) / slices;
+  per = std::min(per, kLatMaxKt);
+  return (ktiles + per - 1) / per;  // no empty slice
+}
+
+size_t x6_lat_part_floats(int rows, int n, int slices) {
+  return (size_t)std::min(rows, kX6LatWindow) * (size_t)n * (size_t)slices;
+}
+
+int launch_gemm_bf16x6_lat(hipStream_t s, const X6Gemm &a, float *part, size_t part_floats) {
+  if (a.tail) a.tail->active = false;
   if (a.m <= 0 || a.n <= 0) return CE_GPU_OK;
-  if (!a.xf || !a.wd || !a.y32 || a.kpad % 32 != 0 || a.din % 8 != 0 || a.din <= 0 || a.nseg < 1 || a.nseg > 8 ||
-      a.nseg * a.din > a.kpad || a.wd_kt * 32 < a.kpad)
+  // the last layer's reduce inside the finalize when the rows are one window
+  const bool reduce = !(a.tail && a.m <= kX6LatWindow && a.n % 4 == 0 && a.n <= 4096 && a.npost <= 4);
+  if (!a.xf || !a.wd || (reduce && !a.y32) || a.kpad % 32 != 0 || a.din % 8 != 0 || a.din <= 0 || a.nseg < 1 ||
+      a.nseg > 8 || a.nseg * a.din > a.kpad || a.wd_kt * 32 < a.kpad)
     return fail(CE_GPU_EINVAL, "gemm_bf16x6 latency: bad K geometry or missing weight fragments");
+  if (!reduce && a.m > kX6LatWindow)
+    return fail(CE_GPU_EINVAL, "gemm_bf16x6 latency: a deferred reduce needs rows <= kX6LatWindow");
   if (a.n % 4 != 0 || a.ldy % 4 != 0 || a.ldx % 4 != 0 || (reinterpret_cast<uintptr_t>(a.xf) & 15) ||
       (reinterpret_cast<uintptr_t>(a.wd) & 15) || a.npost > 4)
     return fail(CE_GPU_EINVAL, "gemm_bf16x6 latency: operands must be 16-byte aligned, widths multiples of 4");
-  Lat2Args p;
+  LatArgs p;
   p.xf = a.xf;
   p.wd = a.wd;
-  p.row_map = a.row_map;
+  p.part = part;
   p.ldx = a.ldx;
   p.wd_kt = a.wd_kt;
   p.m = a.m;
@@ -222,28 +414,97 @@ int launch_gemm_bf16x6_lat(hipStream_t s, const X6Gemm &a) {
   p.kpad = a.kpad;
   p.din = a.din;
   p.nseg = a.nseg;
+  p.row_map = a.row_map;
   p.off_packed = 0;
   for (int i = 0; i < a.nseg; ++i) {
     if (a.off[i] < -128 || a.off[i] > 127) return fail(CE_GPU_ENOTSUP, "gemm_bf16x6: splice offset beyond +-127");
     p.off_packed |= (uint64_t)(uint8_t)(int8_t)a.off[i] << (8 * i);
   }
-  p.per = (a.kpad / 32 + kL2Waves - 1) / kL2Waves;
-  p.tiles_n = (a.n + 15) / 16;
-  p.bias = a.bias;
-  p.bn_scale = a.bn_scale;
-  p.bn_offset = a.bn_offset;
-  for (int i = 0; i < 4; ++i) p.post[i] = a.post[i];
-  p.npost = a.npost;
-  p.y = a.y32;
-  p.ldy = a.ldy;
-  const int mode = post_mode(a.post, a.npost);
-  // the row tile fitting the block count (results do not depend on it):
-  // streaming chunks get 16-row tiles, whole utterances 64-row tiles that
-  // reuse each weight fragment four times
-  if (a.m <= 128)
-    launch_lat2<1>(s, p, mode);
+  p.slices = x6_lat_slices(a.kpad, a.n);
+  p.per = (a.kpad / 32 + p.slices - 1) / p.slices;
+  p.tiles_n = (a.n + kLatBW - 1) / kLatBW;
+  LatReduceArgs r;
+  r.part = part;
+  r.bias = a.bias;
+  r.bn_scale = a.bn_scale;
+  r.bn_offset = a.bn_offset;
+  r.y = a.y32;
+  r.slices = p.slices;
+  r.n = a.n;
+  r.ldy = a.ldy;
+  for (int i = 0; i < 4; ++i) r.post[i] = a.post[i];
+  r.npost = a.npost;
+  r.post_mode = post_mode(a.post, a.npost);
+  for (int r0 = 0; r0 < a.m; r0 += kX6LatWindow) {
+    p.row0 = r.row0 = r0;
+    p.rows = r.rows = std::min(kX6LatWindow, a.m - r0);
+    if ((size_t)p.rows * a.n * p.slices > part_floats || !part)
+      return fail(CE_GPU_EINVAL, "gemm_bf16x6 latency: partial workspace too small");
+    // the frame tile fitting the block (results do not depend on it)
+    if (p.rows <= 32)
+      launch_lat_gemm<2>(s, p);
+    else if (p.rows <= 80)
+      launch_lat_gemm<5>(s, p);
+    else
+      launch_lat_gemm<4>(s, p);  // many row tiles: 64-row tiles, two blocks per CU
+    CE_HIP(hipGetLastError());
+    if (!reduce) {
+      LatTail &t = *a.tail;
+      t.active = true;
+      t.part = part;
+      t.slices = p.slices;
+      t.m = a.m;
+      t.n = a.n;
+      t.bias = a.bias;
+      t.bn_scale = a.bn_scale;
+      t.bn_offset = a.bn_offset;
+      for (int i = 0; i < 4; ++i) t.post[i] = a.post[i];
+      t.npost = a.npost;
+      break;
+    }
+    const int64_t threads = (int64_t)p.rows * (a.n / 4);
+    const dim3 grid((unsigned)((threads + 63) / 64)), block(64);
+    switch (r.post_mode) {
+      case kPostModeNone: hipLaunchKernelGGL(lat_reduce_kernel<kPostModeNone>, grid, block, 0, s, r); break;
+      case kPostModeRelu: hipLaunchKernelGGL(lat_reduce_kernel<kPostModeRelu>, grid, block, 0, s, r); break;
+      case kPostModeBn: hipLaunchKernelGGL(lat_reduce_kernel<kPostModeBn>, grid, block, 0, s, r); break;
+      case kPostModeReluBn: hipLaunchKernelGGL(lat_reduce_kernel<kPostModeReluBn>, grid, block, 0, s, r); break;
+      case kPostModeBnRelu: hipLaunchKernelGGL(lat_reduce_kernel<kPostModeBnRelu>, grid, block, 0, s, r); break;
+      default: hipLaunchKernelGGL(lat_reduce_kernel<kPostModeGeneric>, grid, block, 0, s, r); break;
+    }
+    CE_HIP(hipGetLastError());
+  }
+  return CE_GPU_OK;
+}
+
+int launch_lat_finalize(hipStream_t s, const LatTail &t, int first, int rows, bool log_softmax,
+                        const float *log_prior, const int *row_dst, float *out) {
+  if (rows <= 0) return CE_GPU_OK;
+  if (!t.active || !t.part || !out || t.n % 4 != 0 || t.n > 4096 || first < 0 || first + rows > t.m ||
+      t.npost > 4 ||
+      ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(log_prior) |
+        reinterpret_cast<uintptr_t>(t.bias) | reinterpret_cast<uintptr_t>(t.bn_scale) |
+        reinterpret_cast<uintptr_t>(t.bn_offset)) & 15))
+    return fail(CE_GPU_EINVAL, "lat_finalize: no deferred tail or bad geometry");
+  const dim3 grid(rows), block(256);
+  auto go = [&](auto ls) {
+    constexpr bool LS = decltype(ls)::value;
+    switch (post_mode(t.post, t.npost)) {
+#define CE_LAT_FIN(M) \
+  case M: hipLaunchKernelGGL((lat_finalize_kernel<LS, M>), grid, block, 0, s, t, first, log_prior, row_dst, out); break;
+      CE_LAT_FIN(kPostModeNone) CE_LAT_FIN(kPostModeRelu) CE_LAT_FIN(kPostModeBn) CE_LAT_FIN(kPostModeReluBn)
+      CE_LAT_FIN(kPostModeBnRelu)
+#undef CE_LAT_FIN
+      default:
+        hipLaunchKernelGGL((lat_finalize_kernel<LS, kPostModeGeneric>), grid, block, 0, s, t, first, log_prior,
+                           row_dst, out);
+        break;
+    }
+  };
+  if (log_softmax)
+    go(std::true_type());
   else
-    launch_lat2<4>(s, p, mode);
+    go(std::false_type());
   CE_HIP(hipGetLastError());
   return CE_GPU_OK;
 }

@@ -4,7 +4,8 @@
 //   src/vector.cc:109-122: x - log(sum exp x), no max shift) fused with the
 //   log-prior subtraction of AcousticModel::ComputeBatch (src/am.cc:108-112)
 //   and the scatter of valid packed rows to their utterance's output rows.
-//   One wave per row; the row is read once into registers.
+//   One block (vector form) or one wave per row; the row is read once into
+//   registers.
 // rowop: stand-alone ReLU / BatchNorm / Softmax / LogSoftmax / Normalize for
 //   layers that do not directly follow a LinearLayer (never emitted by the
 //   reference's converter, but legal NN02).
@@ -68,58 +69,54 @@ __global__ __launch_bounds__(256) void finalize_kernel(const float *__restrict__
   }
 }
 
-// The same with 16-byte accesses (dim, ldx multiples of 4, aligned rows):
-// lane l holds float4 chunks l, l + 64, ... of its row.
-constexpr int kMaxVecPerLane = 16;  // rows up to 4096 wide
-
-// One row: load(c) gives float4 chunk c of the row's values.
-template <bool LOGSM, class Load>
-__device__ __forceinline__ void finalize_row_vec(Load &&load, int dim, const float *__restrict__ prior, float *o_row,
-                                                 int lane) {
-  float4 *o = reinterpret_cast<float4 *>(o_row);
-  const float4 *pr = reinterpret_cast<const float4 *>(prior);
-  const int d4 = dim >> 2;
-  float4 v[kMaxVecPerLane], pv[kMaxVecPerLane];
-  float s = 0.0f;
-  // the prior's chunks loaded up front with the row (branch-free, clamped),
-  // so the stores below wait on nothing
-  if (prior) {
-#pragma unroll
-    for (int j = 0; j < kMaxVecPerLane; ++j) pv[j] = pr[min(lane + 64 * j, d4 - 1)];
-  }
-#pragma unroll
-  for (int j = 0; j < kMaxVecPerLane; ++j) {
-    const int c = lane + 64 * j;
-    v[j] = c < d4 ? load(c) : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (LOGSM && c < d4) s += expf(v[j].x) + expf(v[j].y) + expf(v[j].z) + expf(v[j].w);
-  }
-  const float ls = LOGSM ? logf(wave_sum(s)) : 0.0f;
-#pragma unroll
-  for (int j = 0; j < kMaxVecPerLane; ++j) {
-    const int c = lane + 64 * j;
-    if (c < d4) {
-      float4 y = v[j];
-      if (LOGSM) y = make_float4(y.x - ls, y.y - ls, y.z - ls, y.w - ls);
-      if (prior) {
-        const float4 p = pv[j];
-        y = make_float4(y.x - p.x, y.y - p.y, y.z - p.z, y.w - p.w);
-      }
-      o[c] = y;
-    }
-  }
-}
+// The same with 16-byte accesses (dim, ldx multiples of 4, aligned rows),
+// one 256-thread block per row: thread t holds float4 chunks t, t + 256, ...
+// of its row (up to 4096 wide), everything loaded up front; the exp sum is
+// per thread in chunk order, then per wave (xor tree), then the four waves'
+// sums in wave order.  A function of the row alone, not of the row count.
+constexpr int kMaxVecPerThread = 4;
 
 template <bool LOGSM>
 __global__ __launch_bounds__(256) void finalize_vec_kernel(const float *__restrict__ x, int ldx, int rows, int dim,
                                                            const float *__restrict__ prior,
                                                            const int *__restrict__ row_dst,
                                                            float *__restrict__ out) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (row >= rows) return;
+  __shared__ float wsum[4];
+  const int row = blockIdx.x, t = threadIdx.x;
   const int dst = row_dst ? row_dst[row] : row;
   if (dst < 0) return;
   const float4 *xr = reinterpret_cast<const float4 *>(x + (int64_t)row * ldx);
-  finalize_row_vec<LOGSM>([&](int c) { return xr[c]; }, dim, prior, out + (int64_t)dst * dim, lane);
+  const float4 *pr = reinterpret_cast<const float4 *>(prior);
+  float4 *o = reinterpret_cast<float4 *>(out + (int64_t)dst * dim);
+  const int d4 = dim >> 2;
+  float4 v[kMaxVecPerThread], pv[kMaxVecPerThread];
+  float s = 0.0f;
+#pragma unroll
+  for (int j = 0; j < kMaxVecPerThread; ++j) {
+    const int c = min(t + 256 * j, d4 - 1);  // clamped: loads branch-free, used only when in range
+    v[j] = xr[c];
+    if (prior) pv[j] = pr[c];
+  }
+  if (LOGSM) {
+#pragma unroll
+    for (int j = 0; j < kMaxVecPerThread; ++j)
+      if (t + 256 * j < d4) s += expf(v[j].x) + expf(v[j].y) + expf(v[j].z) + expf(v[j].w);
+    s = wave_sum(s);
+    if ((t & 63) == 0) wsum[t >> 6] = s;
+    __syncthreads();
+    s = ((wsum[0] + wsum[1]) + wsum[2]) + wsum[3];
+  }
+  const float ls = LOGSM ? logf(s) : 0.0f;
+#pragma unroll
+  for (int j = 0; j < kMaxVecPerThread; ++j) {
+    const int c = t + 256 * j;
+    if (c < d4) {
+      float4 y = v[j];
+      if (LOGSM) y = make_float4(y.x - ls, y.y - ls, y.z - ls, y.w - ls);
+      if (prior) y = make_float4(y.x - pv[j].x, y.y - pv[j].y, y.z - pv[j].z, y.w - pv[j].w);
+      o[c] = y;
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void rowop_kernel(int kind, float *__restrict__ x, int ldx, int rows,
@@ -230,14 +227,16 @@ int launch_finalize(hipStream_t s, const float *x, int ldx, int rows, int dim, b
                     const float *log_prior, const int *row_dst, float *out) {
   if (rows <= 0) return CE_GPU_OK;
   dim3 grid((rows + 3) / 4), block(256);
-  const bool vec = dim % 4 == 0 && ldx % 4 == 0 && dim <= 4 * 64 * kMaxVecPerLane &&
+  const bool vec = dim % 4 == 0 && ldx % 4 == 0 && dim <= 4 * 256 * kMaxVecPerThread &&
                    ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(out) |
                      reinterpret_cast<uintptr_t>(log_prior)) & 15) == 0;
   if (vec) {
     if (log_softmax)
-      hipLaunchKernelGGL(finalize_vec_kernel<true>, grid, block, 0, s, x, ldx, rows, dim, log_prior, row_dst, out);
+      hipLaunchKernelGGL(finalize_vec_kernel<true>, dim3(rows), block, 0, s, x, ldx, rows, dim, log_prior, row_dst,
+                         out);
     else
-      hipLaunchKernelGGL(finalize_vec_kernel<false>, grid, block, 0, s, x, ldx, rows, dim, log_prior, row_dst, out);
+      hipLaunchKernelGGL(finalize_vec_kernel<false>, dim3(rows), block, 0, s, x, ldx, rows, dim, log_prior, row_dst,
+                         out);
     CE_HIP(hipGetLastError());
     return CE_GPU_OK;
   }

@@ -64,7 +64,7 @@ def test_product_library_has_no_ablation_kernels():
     i8 = re.findall(rb"gemm_i8_glds_kernelILi\d+ELi\d+ELi\d+ELi\d+ELi\d+ELi\d+ELi(\d+)E", data)
     assert i8, "no int8 LDS-DMA GEMM found"
     assert set(i8) == {b"0"}, sorted(set(i8))
-    assert b"gemm_i8_pipe_kernel" in data and b"lat2_kernel" in data
+    assert b"gemm_i8_pipe_kernel" in data and b"lat_gemm_kernel" in data
     assert b"gemm_bf16x6r_kernel" not in data
 
 

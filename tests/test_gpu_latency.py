@@ -1,11 +1,16 @@
-"""Latency mode (ce_gpu_ctx_set_latency, kernels/gemm_bf16x6_lat.hip): one
-launch per layer with 16-unit output tiles, so a small row block -- the
-streaming AcousticModel::Process chunk (src/am.cc:115-142) or one utterance
--- spreads over the chip; K is split over each block's four waves (a
-function of K only) and the partial tiles are summed in wave order in LDS.
-Same bars as the default mode: log-likelihoods within 1e-4 of the oracle,
-bit-identical across row segmentations, row-tile shapes and batchings, and
-deterministic run to run (no atomics, no inter-block hand-off)."""
+"""Latency mode (ce_gpu_ctx_set_latency, kernels/gemm_bf16x6_lat.hip): small
+row blocks -- the streaming AcousticModel::Process chunk (src/am.cc:115-142)
+or one utterance -- spread over the chip by splitting each layer's K over
+64-unit x 80-row blocks (a split chosen from the layer's shape only); the
+blocks' partials are summed in split order by a reduce launch, or, for the
+last layer, inside the finalize.  Same bars as the default mode:
+log-likelihoods within 1e-4 of the oracle, bit-identical across row
+segmentations, row groupings and batchings, and deterministic run to run (no
+atomics, no inter-block hand-off)."""
+import os
+import subprocess
+import sys
+
 import numpy as np
 import pytest
 
@@ -114,3 +119,34 @@ def test_latency_long_block_windows(torch, G, lctx, oracle, xs_config):
     lo, hi = 2048 - 30, 2048 + 30
     want = oracle.nnet_propagate(am["layers"], x[lo:hi + ctx_rows])
     assert np.abs(got[lo:hi] - want).max() <= LOGLIK_TOL
+
+
+FUSED_CHILD = r"""
+import sys, numpy as np, torch
+from catears_amd import gpu
+ctx = gpu.Context(0)
+ctx.set_latency(True)
+model = gpu.Model(ctx, sys.argv[1])
+outs = []
+for rows, seed in ((70, 760), (1018, 761)):
+    x = np.random.default_rng(seed).normal(0.0, 3.0, size=(rows, 40)).astype(np.float32)
+    outs.append(gpu.nnet_propagate(ctx, model, torch.from_numpy(x).to("cuda:0"), subtract_prior=True).cpu().numpy())
+np.save(sys.argv[2], np.concatenate(outs))
+"""
+
+
+def test_latency_fused_final_reduce_exact(tmp_path, s_config):
+    """The last layer's split-K reduce run inside the finalize (the default)
+    gives the bits of its own reduce launch followed by the finalize
+    (CATEARS_LAT_FUSED_FINAL=0)."""
+    from conftest import ROOT
+    got = {}
+    for flag in ("1", "0"):
+        env = dict(os.environ, CATEARS_LAT_FUSED_FINAL=flag, PYTHONPATH=ROOT)
+        path = tmp_path / f"f{flag}.npy"
+        r = subprocess.run([sys.executable, "-c", FUSED_CHILD, s_config, str(path)], env=env, capture_output=True,
+                           text=True, timeout=300, cwd=ROOT)
+        assert r.returncode == 0, r.stderr[-3000:]
+        got[flag] = np.load(path).view(np.uint32)
+    assert got["1"].size > 0
+    assert np.array_equal(got["1"], got["0"])

@@ -52,6 +52,9 @@ def test_x6_variants_bit_identical(tmp_path, s_config):
     # against the round-3 splice_pad launch before it (CATEARS_X6_FIRST=0)
     padded = _run(0, s_config, tmp_path / "pad.npy", CATEARS_X6_FIRST="0")
     assert np.array_equal(padded, base), "the gathered first layer differs from splice_pad"
+    # the gathered first layer on the hidden layers' 256 x 128 tiles
+    wide = _run(0, s_config, tmp_path / "t256.npy", CATEARS_X6_FIRST_TILE="256")
+    assert np.array_equal(wide, base), "the first layer's 256-unit tiles differ"
 
 
 def test_unknown_variant_fails_loudly(tmp_path, s_config):
