@@ -106,8 +106,8 @@ __global__ __launch_bounds__(64 * kLatNW, MULTI && TF == 4 && KT <= 6 ? 2 : 1) v
   // a wait on it would otherwise wait on the weights too), then every load
   // (branch-free, so all of a thread's loads are in flight together), then the
   // splits and LDS stores.  A chunk's 8 k lie in one segment (din % 8 == 0);
-  // k past the segments is K's zero padding; tasks past the slice load a
-  // clamped (valid) address.
+  // k past the segments is K's zero padding, loaded from column 0 of the
+  // clamped row; tasks past the slice load a clamped (valid) address.
   constexpr int NT = 64 * kLatNW, TASKS = KT * BF * 4, TPT = (TASKS + NT - 1) / NT;
   gvec *xptr[TPT];
   bool xlive[TPT];
@@ -122,8 +122,11 @@ __global__ __launch_bounds__(64 * kLatNW, MULTI && TF == 4 && KT <= 6 ? 2 : 1) v
       const int seg = k / p.din, segc = min(seg, p.nseg - 1);
       const int shift = (int)(signed char)(p.off_packed >> (8 * segc));
       xrow[j] = clampi(clampi(f0 + prow, 0, p.m - 1) + shift, 0, p.m - 1);
-      xcol[j] = k - segc * p.din;
       xlive[j] = tid + j * NT < TASKS && i < nk && seg < p.nseg && !(DIAG & 2);
+      // a dead task (K padding past the segments, past the slice or the
+      // task count) reads column 0 of its clamped row: never past the end
+      // of the row, so never past the end of the caller's buffer
+      xcol[j] = seg < p.nseg ? k - segc * p.din : 0;
     }
     if (p.row_map) {
 #pragma unroll

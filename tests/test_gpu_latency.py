@@ -150,3 +150,24 @@ def test_latency_fused_final_reduce_exact(tmp_path, s_config):
         got[flag] = np.load(path).view(np.uint32)
     assert got["1"].size > 0
     assert np.array_equal(got["1"], got["0"])
+
+
+def test_first_layer_reads_stay_inside_the_input(torch, G, lctx, xs_config):
+    """The first layer reads the caller's 40-wide rows directly; its K
+    padding (5 x 40 = 200 of 224 / 256) loads column 0 of a valid row, never
+    past the row.  The input here ends exactly at the end of a
+    2 MiB allocation; both modes give the bits of the same rows scored from
+    an ordinary tensor."""
+    model = G.Model(lctx, xs_config)
+    tctx = G.Context(0)
+    tmodel = G.Model(tctx, xs_config)
+    rows = 70
+    n = 2 * 1024 * 1024 // 4
+    buf = torch.empty(n, dtype=torch.float32, device="cuda")
+    x = buf[n - rows * 40:].view(rows, 40)
+    host = np.random.default_rng(770).normal(0.0, 3.0, size=(rows, 40)).astype(np.float32)
+    x.copy_(torch.from_numpy(host))
+    for c, m in ((lctx, model), (tctx, tmodel)):
+        got = G.nnet_propagate(c, m, x).cpu().numpy()
+        want = G.nnet_propagate(c, m, dev(torch, host)).cpu().numpy()
+        assert np.array_equal(bits(got), bits(want))
