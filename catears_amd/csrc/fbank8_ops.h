@@ -43,7 +43,15 @@ namespace fb8 {
 constexpr int kLanes = 8;    // lanes per frame
 constexpr int kPts = 32;     // complex points per lane
 constexpr int kSamp = 25;    // sample pairs per lane (400 samples / 8 lanes / 2)
-constexpr int kStride = 264; // floats per frame in LDS (256 points + 8: frames on distinct banks)
+// Floats per frame in LDS: 256 points + 12.  The frames of a 32-lane group
+// (4 frames x 8 lanes) start 12 banks apart, so the post-pass power stores
+// (a frame's lanes 16 floats apart) land on 8 banks instead of 4: C2 exact
+// 1.018-1.022 -> 1.040-1.048 G frames/s against 264 (260: 1.005-1.013;
+// tools/experiments/gpu_r4e.sh).  Any value >= 260 gives the same bits.
+#ifndef FB8_STRIDE
+#define FB8_STRIDE 268
+#endif
+constexpr int kStride = FB8_STRIDE;
 constexpr int kOpsA = 23;    // phase-A node ops per lane
 constexpr int kTwA = 8;      // floats per phase-A twiddle record (6 used)
 
