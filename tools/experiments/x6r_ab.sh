@@ -1,7 +1,10 @@
 # bf16x6 default (0 = 300, direct weights + LDS activations) vs 400
 # (register-direct, no LDS): C3 at the driver's step counts, alternating,
-# then serial per-layer launch times.
+# then serial per-layer launch times.  Variant 400 lives in the experiments
+# build only (`make EXPERIMENTS=1 lib`; remove its line from .gpurunignore
+# for the call): both variants run from that library.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
+export CATEARS_HIP_LIB=$R/catears_amd/lib/libcatears_hip_exp.so
 cd "$R" && mkdir -p gpurun_out/x6r
 for rep in 1 2 3; do
   for v in 0 400; do
