@@ -33,7 +33,7 @@ KERNELS := $(wildcard $(SRC)/kernels/*.hip)
 HOSTSRC := $(SRC)/capi.cc $(SRC)/tables.cc
 OBJS := $(patsubst $(SRC)/kernels/%.hip,$(OBJ)/%.o,$(KERNELS)) \
         $(patsubst $(SRC)/%.cc,$(OBJ)/%.o,$(HOSTSRC))
-HDRS := include/catears_gpu.h $(SRC)/internal.h $(SRC)/fbank_ops.h $(SRC)/tile_order.h $(SRC)/lds_dma.h
+HDRS := include/catears_gpu.h $(SRC)/internal.h $(SRC)/fbank_ops.h $(SRC)/fbank8_ops.h $(SRC)/tile_order.h $(SRC)/lds_dma.h
 
 all: $(LIB) oracle
 
