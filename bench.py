@@ -275,11 +275,16 @@ def pmc_mfma(kernel, workload="c3"):
     if hits:
         n = sum(v["dispatches"] for v in hits)
         avg = lambda key: round(sum(v[key] * v["dispatches"] for v in hits) / n, 4)
-        if True:
-            return {"chip": avg("mfma_util_chip"), "active_cus": avg("mfma_util_active_cus"),
-                    "source": os.path.relpath(files[-1], ROOT),
-                    "definition": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 x SIMDs), serial run: chip = "
-                                  "1024 SIMDs, active_cus = 4 x the CUs the grid occupies"}
+        out = {"chip": avg("mfma_util_chip"), "active_cus": avg("mfma_util_active_cus"),
+               "source": os.path.relpath(files[-1], ROOT),
+               "definition": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 x SIMDs), serial run: chip = "
+                             "1024 SIMDs, active_cus = 4 x the CUs the grid occupies; dispatch-weighted over "
+                             "the instantiations in `per_instantiation`"}
+        if len(hits) > 1:
+            out["per_instantiation"] = {
+                name.replace("catears::", ""): {"dispatches": v["dispatches"], "active_cus": v["mfma_util_active_cus"]}
+                for name, v in data["kernels"].items() if kernel_match(name, kernel)}
+        return out
     return None
 
 
