@@ -46,6 +46,42 @@ def main(calls=200):
                                      "sha1": digest}
             print(f"{mode:10s} rows {rows:5d}: {us:8.1f} us/call  {frames / us * 1e6 / 1e6:7.3f} M frames/s"
                   f"  out {digest}", flush=True)
+    if os.environ.get("LAT_GRAPH"):
+        # the same calls captured once in a HIP graph (fixed input / output
+        # buffers) and replayed: the launch cost of a serving loop that stages
+        # each chunk into the captured input
+        for mode in modes:
+            s = torch.cuda.Stream()
+            ctx = gpu.Context(0, s)
+            ctx.set_latency(mode == "latency")
+            model = gpu.Model(ctx, conf)
+            for rows in sizes:
+                x = torch.from_numpy(np.random.default_rng(rows).normal(0, 3, size=(rows, 40))
+                                     .astype(np.float32)).cuda()
+                with torch.cuda.stream(s):
+                    out = gpu.nnet_propagate(ctx, model, x)
+                    for _ in range(3):
+                        gpu.nnet_propagate(ctx, model, x, out=out)
+                s.synchronize()
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s):
+                    gpu.nnet_propagate(ctx, model, x, out=out)
+                for _ in range(20):
+                    g.replay()
+                torch.cuda.synchronize()
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                for _ in range(calls):
+                    g.replay()
+                b.record()
+                torch.cuda.synchronize()
+                us = a.elapsed_time(b) * 1e3 / calls
+                frames = rows - model.left - model.right
+                digest = hashlib.sha1(out.cpu().numpy().tobytes()).hexdigest()[:12]
+                res[f"graph-{mode}/{rows}"] = {"us_per_call": round(us, 1), "frames_per_s": round(frames / us * 1e6),
+                                               "sha1": digest}
+                print(f"graph {mode:10s} rows {rows:5d}: {us:8.1f} us/call  {frames / us * 1e6 / 1e6:7.3f} M frames/s"
+                      f"  out {digest}", flush=True)
     print(json.dumps(res))
 
 
