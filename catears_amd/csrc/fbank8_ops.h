@@ -348,10 +348,19 @@ CE_HD void lane_window(const Sample *src, float mean, int r, const float *win, f
 
 // ------------------------------------------------------- LDS exchanges --
 
+// LDS position of FFT point p during the two transposes (phase A -> B and
+// phase B -> post-pass): four floats of padding after every 64 points.  The
+// sixteen 16-point blocks then start on sixteen distinct 4-bank groups, so a
+// frame's eight lanes reading or writing one block each (load_b / store_b)
+// never share a bank (without it the 16-point blocks started on 4 bank
+// groups: 3-way conflicts).  Points 0..255 -> 0..267: the 268-float frame.
+// Every access below stays a lane base plus an immediate.
+CE_HD constexpr int tpos(int p) { return p + 4 * (p >> 6); }
+
 // phase A -> LDS: lane r's point r + 8j from register j
 CE_HD void store_a(const float *v, int r, float *fbuf) {
   CE_UNROLL
-  for (int j = 0; j < kPts; ++j) fbuf[r + 8 * j] = v[j];
+  for (int j = 0; j < kPts; ++j) fbuf[r + tpos(8 * j)] = v[j];  // (r + 8j) >> 6 = j >> 3
 }
 
 // four floats at a 16-byte aligned LDS address (one ds_read/write_b128)
@@ -363,14 +372,14 @@ struct alignas(16) F4 {
 CE_HD void load_b(int q, const float *fbuf, float *v) {
   CE_UNROLL
   for (int j = 0; j < kPts; j += 4) {
-    const F4 t = *reinterpret_cast<const F4 *>(fbuf + phase_b_point(q, j));
+    const F4 t = *reinterpret_cast<const F4 *>(fbuf + tpos(phase_b_point(q, j)));
     v[j] = t.x, v[j + 1] = t.y, v[j + 2] = t.z, v[j + 3] = t.w;
   }
 }
 CE_HD void store_b(int q, const float *v, float *fbuf) {
   CE_UNROLL
   for (int j = 0; j < kPts; j += 4)
-    *reinterpret_cast<F4 *>(fbuf + phase_b_point(q, j)) = F4{v[j], v[j + 1], v[j + 2], v[j + 3]};
+    *reinterpret_cast<F4 *>(fbuf + tpos(phase_b_point(q, j))) = F4{v[j], v[j + 1], v[j + 2], v[j + 3]};
 }
 
 // the post-pass operands of lane q's slots: B_k and B_{256-k} (bit-reversed
@@ -381,11 +390,13 @@ CE_HD void load_post(int q, const float *fbuf, float *x, float *y) {
   // bitrev8(post_k(q, t)) and bitrev8(256 - post_k(q, t)) as a lane base and
   // a constant (post_k); slot 15 (k = 16 (q + 1)) from its own lane terms
   // (offsets non-negative: an LDS instruction's offset field is unsigned)
+  // (the tpos padding of those points is a constant per t: 2 brev3(q) < 16
+  // never carries across a 64-point boundary)
   const float *bx = fbuf + (brev3(q) << 1), *by = fbuf + 15 - (brev3(q) << 1);
   CE_UNROLL
   for (int t = 0; t < 15; ++t) {
-    x[t] = bx[brev4(t + 1) << 4];
-    y[t] = by[240 - (brev4(t) << 4)];
+    x[t] = bx[tpos(brev4(t + 1) << 4)];
+    y[t] = by[tpos(255 - (brev4(t) << 4)) - 15];
   }
   x[15] = fbuf[brev4(q + 1)];
   y[15] = fbuf[brev4(15 - q)];
