@@ -171,3 +171,51 @@ def test_first_layer_reads_stay_inside_the_input(torch, G, lctx, xs_config):
         got = G.nnet_propagate(c, m, x).cpu().numpy()
         want = G.nnet_propagate(c, m, dev(torch, host)).cpu().numpy()
         assert np.array_equal(bits(got), bits(want))
+
+
+POST_CHILD = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[2])
+from test_gpu_latency import post_model_layers
+from catears_amd import gpu, formats
+layers, left, right, prior = post_model_layers()
+ctx = gpu.Context(0)
+ctx.set_latency(True)
+model = gpu.Model(ctx, image=formats.nnet_bytes(layers, left, right), prior=prior)
+x = np.random.default_rng(763).normal(0.0, 3.0, size=(70, 40)).astype(np.float32)
+np.save(sys.argv[1], gpu.nnet_propagate(ctx, model, torch.from_numpy(x).to("cuda:0")).cpu().numpy())
+"""
+
+
+def post_model_layers():
+    """TDNN-XS with ReLU + BatchNorm after its last Linear (legal NN02): the
+    last GEMM carries post ops, so the fused finalize applies them."""
+    from catears_amd import synth
+    layers, left, right, prior = synth.tdnn_layers(256, 512, seed=21)
+    last = layers.pop()
+    rng = np.random.default_rng(5)
+    layers += [{"kind": "relu"},
+               {"kind": "batchnorm", "scale": (1.0 + 0.1 * rng.uniform(-1, 1, 512)).astype(np.float32),
+                "offset": (0.1 * rng.uniform(-1, 1, 512)).astype(np.float32)},
+               last]
+    return layers, left, right, prior
+
+
+def test_latency_fused_final_with_post_ops(tmp_path, oracle):
+    """A last Linear followed by ReLU + BatchNorm: the fused finalize (the
+    default) gives the bits of its own reduce launch and the finalize, and
+    the oracle's values."""
+    from conftest import ROOT
+    got = {}
+    for flag in ("1", "0"):
+        env = dict(os.environ, CATEARS_LAT_FUSED_FINAL=flag, PYTHONPATH=ROOT)
+        path = tmp_path / f"p{flag}.npy"
+        r = subprocess.run([sys.executable, "-c", POST_CHILD, str(path), os.path.join(ROOT, "tests")], env=env,
+                           capture_output=True, text=True, timeout=300, cwd=ROOT)
+        assert r.returncode == 0, r.stderr[-3000:]
+        got[flag] = np.load(path)
+    assert np.array_equal(bits(got["1"]), bits(got["0"]))
+    layers, _, _, _ = post_model_layers()
+    x = np.random.default_rng(763).normal(0.0, 3.0, size=(70, 40)).astype(np.float32)
+    want = oracle.nnet_propagate(layers, x, gemm=lambda a, w: a @ w)
+    assert np.abs(got["1"] - want).max() <= LOGLIK_TOL
