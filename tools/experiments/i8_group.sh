@@ -1,6 +1,6 @@
 # int8 GEMM XCD tile-group width (CATEARS_I8_GROUP): serial hidden-layer
-# (CATEARS_I8_GROUP was a measurement build's knob; the product library fixes the group at 8.)
 # time under rocprofv3 and C5 at 20 steps.
+# (CATEARS_I8_GROUP was a measurement build's knob; the product library fixes the group at 8.)
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" && mkdir -p gpurun_out/i8g
 O=gpurun_out/i8g
