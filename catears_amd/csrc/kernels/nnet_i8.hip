@@ -428,7 +428,14 @@ __device__ __forceinline__ void i8_epilogue_v(const I8Args &p, const i32x16 (&ac
         const int idx = lane + 64 * q, rr = idx / C4, c4 = idx % C4;
         const int row = m0 + wrow + i * 32 + rr, col = col0 + 4 * c4;
         const float4 v = *reinterpret_cast<const float4 *>(slab + rr * SW + 4 * c4);
-        if (row < p.m && col < p.n) *reinterpret_cast<float4 *>(p.y + (int64_t)row * p.ldy + col) = v;
+        // non-temporal: the next layer's Quantize reads it once, later
+        // (serial hidden layer 36.8-37.0 -> 35.3-35.8 us, Quantize +0.4 us;
+        // tools/experiments/i8_nt.sh)
+        if (row < p.m && col < p.n) {
+          typedef float nt4 __attribute__((ext_vector_type(4)));
+          __builtin_nontemporal_store(nt4{v.x, v.y, v.z, v.w},
+                                      reinterpret_cast<nt4 *>(p.y + (int64_t)row * p.ldy + col));
+        }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
