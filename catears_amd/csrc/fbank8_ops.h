@@ -348,19 +348,21 @@ CE_HD void lane_window(const Sample *src, float mean, int r, const float *win, f
 
 // ------------------------------------------------------- LDS exchanges --
 
-// LDS position of FFT point p during the two transposes (phase A -> B and
-// phase B -> post-pass): four floats of padding after every 64 points.  The
-// sixteen 16-point blocks then start on sixteen distinct 4-bank groups, so a
-// frame's eight lanes reading or writing one block each (load_b / store_b)
-// never share a bank (without it the 16-point blocks started on 4 bank
-// groups: 3-way conflicts).  Points 0..255 -> 0..267: the 268-float frame.
-// Every access below stays a lane base plus an immediate.
+// LDS position of FFT point p during the phase B -> post-pass transpose:
+// four floats of padding after every 64 points.  The sixteen 16-point
+// blocks then start on sixteen distinct 4-bank groups, so a frame's eight
+// lanes writing one block each (store_b) never share a bank (without it the
+// blocks started on 4 bank groups: 3-way conflicts).  Points 0..255 ->
+// 0..267: the 268-float frame.  The phase A -> B transpose keeps the plain
+// positions: with the guide's lane groups for ds_read_b128 its load_b
+// conflicts less that way (tools/fb_bank_model.py: 96 vs 160 extra passes
+// per group).  Every access below stays a lane base plus an immediate.
 CE_HD constexpr int tpos(int p) { return p + 4 * (p >> 6); }
 
 // phase A -> LDS: lane r's point r + 8j from register j
 CE_HD void store_a(const float *v, int r, float *fbuf) {
   CE_UNROLL
-  for (int j = 0; j < kPts; ++j) fbuf[r + tpos(8 * j)] = v[j];  // (r + 8j) >> 6 = j >> 3
+  for (int j = 0; j < kPts; ++j) fbuf[r + 8 * j] = v[j];
 }
 
 // four floats at a 16-byte aligned LDS address (one ds_read/write_b128)
@@ -372,7 +374,7 @@ struct alignas(16) F4 {
 CE_HD void load_b(int q, const float *fbuf, float *v) {
   CE_UNROLL
   for (int j = 0; j < kPts; j += 4) {
-    const F4 t = *reinterpret_cast<const F4 *>(fbuf + tpos(phase_b_point(q, j)));
+    const F4 t = *reinterpret_cast<const F4 *>(fbuf + phase_b_point(q, j));
     v[j] = t.x, v[j + 1] = t.y, v[j + 2] = t.z, v[j + 3] = t.w;
   }
 }
