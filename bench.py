@@ -82,6 +82,9 @@ def parse(argv=None):
     ap.add_argument("--c4-dump", default=None,
                     help="c4, tests only: rank 0 writes every gathered row (and its own) per utterance "
                          "to this .npz (small corpora)")
+    ap.add_argument("--c4-dump-every", type=int, default=1,
+                    help="c4 with --c4-dump on one process: keep only utterances u with u %% K == 0 (the full "
+                         "corpus, sampled)")
     ap.add_argument("--host-io", action="store_true",
                     help="c3: the PCIe-inclusive rate of a host-side caller -- every step's PCM is copied from "
                          "pinned host memory and its log-likelihoods back to pinned host memory, on copy streams "
@@ -529,6 +532,7 @@ def main_c4(args):
     done = [None] * nbuf
     gather = world > 1 and not args.no_gather
     dump = {} if (args.c4_dump and rank == 0) else None
+    assert args.c4_dump_every == 1 or world == 1, "--c4-dump-every samples one process's own batches only"
     gat = RowGather(counts, pdfs, torch.float32, "cuda", depth=nbuf, keep=dump is not None) if gather else None
     comm = torch.cuda.Stream() if gather else None
     checksum = torch.zeros((), dtype=torch.float64, device="cuda")
@@ -569,9 +573,9 @@ def main_c4(args):
             # one process: consume every row the same way rank 0 does
             with torch.cuda.stream(stream):
                 checksum.add_(torch.sum(outs[o][:n], dtype=torch.float64))
-        if dump is not None and (rank == 0):
+        if dump is not None and (rank == 0) and any(int(u) % args.c4_dump_every == 0 for u in batches[i]):
             stream.synchronize()
-            _c4_keep(dump, batches[i], frames, outs[o][:n].cpu().numpy())
+            _c4_keep(dump, batches[i], frames, outs[o][:n].cpu().numpy(), args.c4_dump_every)
 
     def idle_step(s):
         # this rank has no batch at step s but peers may (rank 0 receives)
@@ -671,11 +675,13 @@ def main_c4(args):
         dist.destroy_process_group()
 
 
-def _c4_keep(dump, utts, frames, rows):
-    """Split a batch's rows (utterances back to back) per utterance."""
+def _c4_keep(dump, utts, frames, rows, every=1):
+    """Split a batch's rows (utterances back to back) per utterance; keep
+    utterances u with u % every == 0."""
     at = 0
     for u in utts:
-        dump[int(u)] = rows[at:at + frames[u]]
+        if int(u) % every == 0:
+            dump[int(u)] = rows[at:at + frames[u]].copy()
         at += frames[u]
     assert at == rows.shape[0]
 

@@ -163,3 +163,47 @@ def test_c4_rows_match_oracle(tmp_path_factory, model, utts):
         assert got.shape == ref.shape == (frames[u], am["log_prior"].shape[0])
         err = float(np.abs(got - ref).max())
         assert err <= 1e-4, (u, err)
+
+
+def test_c4_full_corpus_sampled_rows_match_oracle(tmp_path):
+    """The whole C4 corpus (36 000 utterances, 100 h, TDNN-S, ~9 000 ragged
+    <= 4096-row batches) in one process, one utterance in 3 000 kept: every
+    kept utterance has its frame count, and four of them -- the shortest,
+    the longest, and the first and last kept -- are within 1e-4 of the
+    oracle (fp64 network).  Exercises the full-size batching the small
+    corpora above do not reach."""
+    import tempfile
+
+    from catears_amd import formats, synth
+    from catears_amd.shard import c4_corpus, num_frames, pack_batches, shard_utterances
+    from oracle import pyoracle
+    every = 3000
+    dump = tmp_path / "full.npz"
+    env = dict(os.environ, PYTHONPATH=ROOT, CATEARS_BENCH_DEVICE="0")
+    r = subprocess.run([sys.executable, "bench.py", "--workload", "c4", "--model", "tdnn-s", "--warmup", "2",
+                        "--no-cpu-baseline", "--c4-dump", str(dump), "--c4-dump-every", str(every)],
+                       env=env, cwd=ROOT, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    conf = synth.write_model(os.path.join(tempfile.gettempdir(), f"catears_bench_{os.getuid()}"), "tdnn-s")
+    am = formats.read_am(conf)
+    samples = c4_corpus(36000)
+    frames = [num_frames(int(n)) for n in samples]
+    batches = pack_batches([frames[u] for u in shard_utterances(frames, 1, 0)], am["left"], am["right"], 4096)
+    assert line["config"]["batches_per_rank"] == [len(batches)] and len(batches) > 8000
+    rows = dict(np.load(dump))
+    kept = sorted(int(k[1:]) for k in rows)
+    assert kept == list(range(0, 36000, every))
+    for u in kept:
+        assert rows[f"u{u}"].shape == (frames[u], am["log_prior"].shape[0]), u
+    by_len = sorted(kept, key=lambda u: samples[u])
+    pick = {by_len[0], by_len[-1], kept[0], kept[-1]}
+    plen = int(samples.max())
+    gstats = synth.cmvn_stats_synthetic()
+    fb = pyoracle.Fbank()
+    f64 = lambda a, w: (a.astype(np.float64) @ w.astype(np.float64)).astype(np.float32)
+    for u in sorted(pick):
+        wave = synth.pcm(600000 + u % 48, plen)[:int(samples[u])]  # bench.py main_c4's resident pool
+        ref = pyoracle.am_whole(am, pyoracle.cmvn(gstats, fb.compute(wave)), gemm=f64)
+        err = float(np.abs(rows[f"u{u}"] - ref).max())
+        assert err <= 1e-4, (u, err)
