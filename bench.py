@@ -381,6 +381,14 @@ def main_c2(args):
         pcm[u].copy_(torch.from_numpy(w.astype(np.int16) if s16 else w))
     pcm = pcm.reshape(-1)
     feats = torch.empty((plan.total_frames, 40), dtype=torch.float32, device="cuda")
+    prewarm_steps = 0
+    torch.cuda.synchronize()
+    tw = time.perf_counter()
+    while (time.perf_counter() - tw) * 1e3 < args.prewarm_ms:  # as main(): the chip settled under load
+        for _ in range(10):
+            gpu.fbank(ctx, plan, pcm, feats)
+        prewarm_steps += 10
+        torch.cuda.synchronize()
     for _ in range(args.warmup):
         gpu.fbank(ctx, plan, pcm, feats)
     torch.cuda.synchronize()
@@ -434,7 +442,8 @@ def main_c2(args):
     line = {
         "metric": "fbank frames/sec (window+SRFFT+mel+log, 25ms/10ms, 40 bins), 16kHz",
         "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4), "higher_is_better": True,
+        "warmup": args.warmup, "prewarm": {"ms": args.prewarm_ms, "steps": prewarm_steps},
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
         "data": "synthetic (seeded 16 kHz PCM at raw int16 scale)",
         "config": {"workload": f"C2 batched fbank only, {n_utt} x {args.seconds:g} s utterances per step per GPU",
