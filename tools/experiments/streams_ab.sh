@@ -1,11 +1,9 @@
-# C3 at the driver's step counts per pipeline shape (front x back streams),
-# alternating, two reps
-set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(pwd)}" && mkdir -p gpurun_out/sab
+#!/bin/bash
+# C3 at the driver's flags (with the pre-warm) for 2, 3 and 4 nnet streams, twice each.
+set -e
+mkdir -p gpurun_out
 for rep in 1 2; do
-  for cfg in "1 3" "1 2" "1 4" "2 3" "2 4"; do
-    set -- $cfg
-    timeout -k 10 200 python bench.py --front-streams $1 --back-streams $2 --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/sab/f$1b$2.$rep.json 2> gpurun_out/sab/f$1b$2.$rep.err || { tail -5 gpurun_out/sab/f$1b$2.$rep.err; exit 1; }
-    python3 -c "import json; d=json.load(open('gpurun_out/sab/f$1b$2.$rep.json')); print('front $1 back $2 rep $rep', round(d['value']/1e6,3), 'M', d['roofline']['frac'])"
-  done
-done
+for nb in 2 3 4; do
+  timeout -k 10 240 python -u bench.py --no-cpu-baseline --steps 20 --warmup 5 --back-streams $nb > gpurun_out/sab_$nb.out 2>/dev/null
+  python -c "import json;d=json.loads(open('gpurun_out/sab_$nb.out').read().strip().splitlines()[-1]);print('nb=$nb',d['value'],d['ms_per_step'])"
+done; done
