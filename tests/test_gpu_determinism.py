@@ -32,3 +32,20 @@ def test_pipelined_batches_equal_serial_rescore(extra):
     assert v["batches"] == 65
     assert v["differing"] == 0, v["detail"]
     assert line["finite"]
+
+
+def test_prewarm_changes_no_result():
+    """The pre-warm (untimed steps before the W warm-up steps) runs the same
+    pipeline on the same inputs: the timed steps' output is bit-identical with
+    and without it, and the line reports it beside `warmup`."""
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    import bench
+    base = ["--steps", "6", "--warmup", "2", "--no-cpu-baseline", "--no-profile"]
+    off = bench.main(base + ["--prewarm-ms", "0"])
+    on = bench.main(base + ["--prewarm-ms", "20"])
+    assert off["prewarm"] == {"ms": 0.0, "steps": 0}
+    assert on["prewarm"]["ms"] == 20.0 and on["prewarm"]["steps"] >= 10
+    assert on["warmup"] == off["warmup"] == 2 and on["steps"] == off["steps"] == 6
+    assert on["checksum"] == off["checksum"]
+    assert on["finite"] and off["finite"]
