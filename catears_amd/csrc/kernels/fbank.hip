@@ -58,7 +58,7 @@ struct Fb8Lds {
   float twa[kOpsA * kLanes * kTwA];
   float win[kWinLen];
   float kn[2 * 129];
-  float melw[kMelWTot * kLanes];
+  alignas(16) float melw[kMelWTot * kLanes];  // read as 16-byte quads (mel_window)
   int mel_st[kMelSlots * kLanes];
 };
 
