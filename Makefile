@@ -23,8 +23,14 @@ endif
 # -ffp-contract=off: the reference's float arithmetic is never fused
 # (x86-64 without FMA); keeping mul/add separate makes the fbank, CMVN and
 # epilogue arithmetic bit-identical to it.  MFMA accumulation is unaffected.
+# No packed-FP32 VALU (v_pk_add/mul/fma_f32, v_pk_mov_b32) in any kernel:
+# under concurrent MFMA kernels on the same CUs their results in lanes 48-63
+# were wrong in ~2 % of fast-fbank launches, and with the feature off in none
+# (tools/experiments/lds_race_stress.py).  The host-side cc1
+# prints "not a recognized feature" for it and ignores it.
+NOPK := -Xclang -target-feature -Xclang -packed-fp32-ops
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -ffp-contract=off \
-            -Iinclude -I$(SRC) -Wall -Wno-unused-function $(EXPFLAGS)
+            -Iinclude -I$(SRC) -Wall -Wno-unused-function $(NOPK) $(EXPFLAGS)
 CXX ?= g++
 HOSTFLAGS := -O2 -fPIC -std=c++17 -ffp-contract=off -Iinclude -I$(SRC) -I/opt/rocm/include \
              -D__HIP_PLATFORM_AMD__ -Wall $(EXPFLAGS)
@@ -53,9 +59,9 @@ $(OBJ)/gemm_bf16x6.o: HIPFLAGS += -fno-slp-vectorize $(X6FLAGS)
 $(OBJ)/fbank.o: HIPFLAGS += -fno-slp-vectorize
 
 # the fast fbank mode is not bit-exact by design: let it contract mul/add
-$(OBJ)/fbank_fast.o: HIPFLAGS += -ffp-contract=fast
+$(OBJ)/fbank_fast.o: HIPFLAGS += -ffp-contract=fast $(FFDIAG)
 
-$(OBJ)/%.o: $(SRC)/kernels/%.hip $(HDRS)
+$(OBJ)/%.o: $(SRC)/kernels/%.hip $(HDRS) Makefile
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -117,6 +117,9 @@ def parse(argv=None):
                          "the library's (bf16x6: three exact bf16 planes, six products, fp32 GEMM)")
     ap.add_argument("--front-streams", type=int, default=1,
                     help="fbank + CMVN streams; consecutive batches alternate between them")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="tests only: start and check the N ranks (self-launch, world size, gloo process group) "
+                         "and print a line with n_gpus and the ranks seen, without touching a GPU")
     ap.add_argument("--back-streams", type=int, default=3,
                     help="nnet streams; consecutive batches alternate between them so one batch's "
                          "wave-quantisation tail overlaps the next batch's layers")
@@ -296,6 +299,76 @@ def pmc_mfma(kernel, workload="c3"):
     return None
 
 
+def launch_ranks(args, argv):
+    """`--gpus N` (N > 1) with no launcher around this process: start the N
+    ranks as ONE child process, `python -m torch.distributed.run
+    --nproc-per-node N bench.py <same arguments>` on 127.0.0.1, echo its
+    output and exit with its return code.  This process has not touched the
+    GPU (no HIP call before here; the children initialise their own devices)
+    and never replaces itself (no exec).  Returns rank 0's JSON line."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env, cwd=ROOT)
+    line = None
+    for ln in p.stdout:
+        sys.stdout.write(ln)
+        sys.stdout.flush()
+        if ln.startswith("{"):
+            try:
+                line = json.loads(ln)
+            except ValueError:
+                pass
+    rc = p.wait()
+    if rc != 0:
+        raise SystemExit(rc)
+    if line is None:
+        raise SystemExit("bench.py: the ranks printed no JSON line")
+    return line
+
+
+def world_of(args):
+    """(rank, world) from the launcher's environment.  The line's n_gpus is
+    the world size, so a run whose world differs from --gpus fails here
+    instead of reporting a mislabelled line."""
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world} (launch N ranks with "
+                         f"torch.distributed.run --nproc-per-node N, or run --gpus N without a launcher)")
+    return rank, world
+
+
+def launch_check(args):
+    """--launch-check: the ranks join a gloo process group and rank 0 prints
+    the world it sees.  No GPU call (the CPU test of the N-rank launch)."""
+    import torch
+    import torch.distributed as dist
+    rank, world = world_of(args)
+    if world > 1:
+        dist.init_process_group("gloo")
+        ranks = [None] * world
+        dist.all_gather_object(ranks, {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", 0)),
+                                       "pid": os.getpid()})
+    else:
+        ranks = [{"rank": 0, "local_rank": 0, "pid": os.getpid()}]
+    line = {"metric": METRIC, "n_gpus": world, "launch_check": True, "ranks": ranks,
+            "torch": torch.__version__}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return line
+
+
 def device_for_rank():
     """LOCAL_RANK's GPU; CATEARS_BENCH_DEVICE pins every rank to one device
     (rehearsing N ranks on a one-GPU box with --dist-backend gloo)."""
@@ -363,8 +436,7 @@ def main_c2(args):
     import torch.distributed as dist
 
     from catears_amd import gpu, synth
-    rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
+    rank, world = world_of(args)
     local = device_for_rank()
     torch.cuda.set_device(local)
     if world > 1:
@@ -478,8 +550,7 @@ def main_c4(args):
     from catears_amd import gpu, synth
     from catears_amd.shard import RowGather, c4_corpus, exchange_counts, num_frames, pack_batches, shard_utterances
 
-    rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
+    rank, world = world_of(args)
     local = device_for_rank()
     torch.cuda.set_device(local)
     if world > 1:
@@ -728,7 +799,19 @@ def verify_serial(args, kept, ctx, model, plan, pcm, gstats, U, pool):
         d_sum = psums.view(torch.int64) != sums.view(torch.int64)
         if bool(d_raw.any()) or bool(d_norm.any()) or bool(d_sum.any()):
             rows = torch.nonzero(d_raw.any(1)).flatten().tolist()
-            bad.append({"step": i, "fbank_rows": rows[:8], "fbank_rows_n": len(rows),
+            # where each differing frame ran: fast mode = 16 lanes per frame,
+            # 4 frames per wave, 4 waves per block; exact = 8 lanes, 8 frames
+            # per wave, 8 waves per block (one grid pass at C3)
+            lanes, fpw, wpb = (16, 4, 4) if args.fbank == "fast" else (8, 8, 8)
+            where = []
+            for r in rows[:4]:
+                bands = torch.nonzero(d_raw[r]).flatten().tolist()
+                g = r % fpw
+                where.append({"row": r, "block": r // (fpw * wpb), "wave": (r // fpw) % wpb, "group": g,
+                              "lanes": [g * lanes, g * lanes + lanes - 1], "bands": bands,
+                              "pipelined": [float(praw[r, b]) for b in bands[:3]],
+                              "serial": [float(raw[r, b]) for b in bands[:3]]})
+            bad.append({"step": i, "fbank_rows": rows[:8], "fbank_rows_n": len(rows), "fbank_where": where,
                         "fbank_bands": [torch.nonzero(d_raw[r]).flatten().tolist() for r in rows[:4]],
                         "cmvn_rows_n": int(d_norm.any(1).sum()), "loglik_rows_n": int(d_sum.sum()),
                         "loglik_first_row": int(torch.nonzero(d_sum).flatten()[0]) if bool(d_sum.any()) else None})
@@ -737,6 +820,11 @@ def verify_serial(args, kept, ctx, model, plan, pcm, gstats, U, pool):
 
 def main(argv=None):
     args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args, sys.argv[1:] if argv is None else argv)
+    world_of(args)
+    if args.launch_check:
+        return launch_check(args)
     if args.workload == "c2":
         return main_c2(args)
     if args.workload == "c4":
@@ -747,11 +835,8 @@ def main(argv=None):
     from catears_amd import gpu, synth
     from catears_amd.shard import RowGather, exchange_counts
 
-    rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
+    rank, world = world_of(args)
     local = device_for_rank()
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     torch.cuda.set_device(local)
     if world > 1:
         init_dist(args, local)

@@ -154,6 +154,23 @@ __device__ __forceinline__ float apply_post(float y, float sc, float of, const i
   return y;
 }
 
+// Cross-lane hand-off through LDS inside one wave (the fbank transposes, the
+// int8 epilogue's row slabs): lanes read what other lanes of the same wave
+// wrote just before, or overwrite what they just read.  The wave waits for
+// all of its LDS operations to complete (lgkmcnt(0)) before it issues the
+// next one; the "memory" clobber keeps the compiler from moving LDS accesses
+// across.  A wavefront-scope fence plus wave_barrier -- the rounds 1-4 form
+// -- emits no wait at all, so it relied on a wave's LDS operations taking
+// effect in issue order.  Under concurrent MFMA-heavy kernels on the same CU
+// that did not hold: reads by the last 16 lanes returned data from before
+// the preceding write (GPUTEST_r04).
+__device__ __forceinline__ void wave_lds_sync() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+#endif
+}
+
 // The latency GEMM's split-K reduce (kernels/gemm_bf16x6_lat.hip): the S
 // slice partials of 4 consecutive outputs (slice s at src + s * stride) summed
 // in slice order, 16 loads in flight at a time.

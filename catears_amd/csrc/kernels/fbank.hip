@@ -42,11 +42,7 @@ constexpr int kFramesPerBlock = 4;  // granularity of the plan's block_utt table
 constexpr int kWaves = FBANK_WAVES;  // waves per block (8 frames each)
 constexpr int kBlocksPerCU = kWaves == 8 ? 2 : 3;  // LDS: kWaves x 8 x 1056 B of frame regions + 11.5 KB of tables
 
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
+__device__ __forceinline__ void wave_sync() { wave_lds_sync(); }
 
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {

@@ -50,17 +50,25 @@ struct FastSmem {
   float mel_w[16 * kFfSlotW];  // FbankTables::ff_slot_w
 };
 
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
+__device__ __forceinline__ void wave_sync() { wave_lds_sync(); }
+
+// FF_DIAG (experiment builds only, tools/experiments/lds_race_stress.py):
+// 1 = the four frames' LDS regions in reverse order, 2 = lane group g
+// computes frame 3 - g, 3 = the row rotates by ds_bpermute instead of DPP
+#ifndef FF_DIAG
+#define FF_DIAG 0
+#endif
 
 // lane j of a 16-lane row receives lane (j - N) mod 16's value (DPP row_ror)
 template <int N>
 __device__ __forceinline__ float row_ror(float v) {
+#if FF_DIAG == 3
+  const int l = __lane_id();
+  return __shfl(v, (l & ~15) | ((l - N) & 15));
+#else
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x120 + N, 0xf, 0xf,
                                                                false));
+#endif
 }
 
 struct Cplx {
@@ -143,7 +151,11 @@ __global__ __launch_bounds__(kWaves * 64, 3) void fbank_fast_kernel(const FbankT
     band[q] = tab->ff_slot_band[q * 16 + j];
     start[q] = tab->ff_slot_start[q * 16 + j];
   }
+#if FF_DIAG == 1
+  float2 *R = sm.frame[wave] + (3 - g) * kRegion;
+#else
   float2 *R = sm.frame[wave] + g * kRegion;  // this frame's LDS region
+#endif
   // the power spectrum reuses the region, 16 dwords in for odd frames: the
   // regions are 544 dwords apart (= 0 mod 32), so frames 2i and 2i+1 -- one
   // 32-lane group of a ds_read_b32 / ds_write_b32 -- would otherwise read and
@@ -151,7 +163,11 @@ __global__ __launch_bounds__(kWaves * 64, 3) void fbank_fast_kernel(const FbankT
   float *P = reinterpret_cast<float *>(R) + 16 * (g & 1);
   const int64_t stride = (int64_t)gridDim.x * kFramesPerBlk;
   for (int64_t fb = ((int64_t)blockIdx.x * kWaves + wave) * kFramesPerWave; fb < total_frames; fb += stride) {
+#if FF_DIAG == 2
+    const int64_t fr = fb + (3 - g);
+#else
     const int64_t fr = fb + g;
+#endif
     const bool active = fr < total_frames;
     const int64_t f = active ? fr : total_frames - 1;  // idle rows recompute the last frame, store nothing
     int u = block_utt[f / 4];  // the exact kernel's 4-frame blocks (ce_gpu_plan_create)

@@ -420,9 +420,7 @@ __device__ __forceinline__ void i8_epilogue_v(const I8Args &p, const i32x16 (&ac
           mn = fminf(mn, rmn[e]);
         }
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      wave_lds_sync();
 #pragma unroll
       for (int q = 0; q < 32 * C4 / 64; ++q) {
         const int idx = lane + 64 * q, rr = idx / C4, c4 = idx % C4;
@@ -437,9 +435,7 @@ __device__ __forceinline__ void i8_epilogue_v(const I8Args &p, const i32x16 (&ac
                                       reinterpret_cast<nt4 *>(p.y + (int64_t)row * p.ldy + col));
         }
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      wave_lds_sync();
     }
     return make_float2(mn, mx);
   });

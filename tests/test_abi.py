@@ -136,3 +136,47 @@ def test_product_kernels_use_no_scratch():
     assert any("fbank_kernel" in k for k in segs)
     scratch = {k: v for k, v in segs.items() if v}
     assert not scratch, scratch
+
+
+def kernel_instruction_counts(path, pattern):
+    """{kernel symbol: count of instructions whose mnemonic matches pattern}
+    from llvm-objdump of the library's gfx950 code objects."""
+    import collections
+    import subprocess
+    import tempfile
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if not os.path.exists(objdump):
+        pytest.skip("llvm-objdump not in this image")
+    rx = re.compile(pattern)
+    out = collections.Counter()
+    n_kernels = 0
+    for co in _code_objects(path):
+        with tempfile.NamedTemporaryFile(suffix=".co") as f:
+            f.write(co)
+            f.flush()
+            asm = subprocess.check_output([objdump, "-d", "--mcpu=gfx950", f.name], text=True)
+        name = None
+        for ln in asm.splitlines():
+            m = re.match(r"^[0-9a-f]+ <(.+)>:", ln)
+            if m:
+                name = m.group(1)
+                n_kernels += 1
+                continue
+            m = re.match(r"^\s+([a-z_0-9]+)", ln)
+            if m and name and rx.fullmatch(m.group(1)):
+                out[name] += 1
+    return out, n_kernels
+
+
+def test_product_kernels_use_no_packed_fp32_valu():
+    """No kernel of the product library issues packed-FP32 VALU instructions
+    (v_pk_add_f32, v_pk_mul_f32, v_pk_fma_f32, v_pk_mov_b32).  With them, the
+    fast fbank kernel's lanes 48-63 computed wrong values in about 2 % of its
+    launches while bf16 MFMA GEMMs ran beside it on other streams (round 4's
+    GPUTEST failure; tools/experiments/lds_race_stress.py: 2 x 126 k launches
+    without a difference once they were gone).  The Makefile
+    builds every kernel with the packed-fp32-ops target feature off."""
+    counts, n = kernel_instruction_counts(os.path.join(ROOT, "catears_amd", "lib", "libcatears_hip.so"),
+                                          r"v_pk_(add|mul|fma)_f32|v_pk_mov_b32")
+    assert n >= 20
+    assert not counts, dict(counts)

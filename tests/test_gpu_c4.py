@@ -37,7 +37,8 @@ def _bench(extra, dump, nproc):
             "--no-cpu-baseline", "--c4-dump", str(dump)] + extra  # (later --model / --c4-utts win)
     if nproc > 1:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(nproc),
-               "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args + ["--dist-backend", "gloo"]
+               "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args + ["--dist-backend", "gloo",
+                                                                                       "--gpus", str(nproc)]
     else:
         cmd = [sys.executable] + args
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=600)
@@ -207,3 +208,20 @@ def test_c4_full_corpus_sampled_rows_match_oracle(tmp_path):
         ref = pyoracle.am_whole(am, pyoracle.cmvn(gstats, fb.compute(wave)), gemm=f64)
         err = float(np.abs(rows[f"u{u}"] - ref).max())
         assert err <= 1e-4, (u, err)
+
+
+def test_c3_gpus_2_self_launched():
+    """`bench.py --gpus 2` with no external launcher: the bench starts its two
+    ranks itself (gloo, both on device 0 here) and the line is a 2-rank line
+    with the gather to rank 0."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(PYTHONPATH=ROOT, CATEARS_BENCH_DEVICE="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--dist-backend", "gloo", "--steps", "6",
+                        "--warmup", "2", "--no-cpu-baseline", "--prewarm-ms", "0"],
+                       env=env, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(line) == 1, r.stdout[-2000:]
+    line = line[0]
+    assert line["n_gpus"] == 2 and line["config"]["gather"] and line["finite"]
+    assert line["value"] > 0
