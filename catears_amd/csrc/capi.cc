@@ -1486,6 +1486,16 @@ static int run_steps(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, int
   return run_steps_f32(ctx, m, x, ldx, rows, row_map, y, ldy);
 }
 
+// The latency GEMM may defer its last layer's reduce into the finalize only
+// when the fused finalize can write the caller's output: it stores 16-byte
+// row chunks (launch_lat_finalize), so out and the log prior must be 16-byte
+// aligned.  Otherwise the layer keeps its own reduce launch and the ordinary
+// finalize (scalar path for unaligned rows) runs -- decided before any GEMM
+// is launched.
+static bool lat_tail_ok(const float *out, const float *log_prior) {
+  return ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(log_prior)) & 15) == 0;
+}
+
 // launch_finalize on rows first .. first + rows - 1 of run_steps' output
 // (or of its deferred latency tail: the last layer's reduce in the same
 // launch)
@@ -1574,7 +1584,8 @@ int ce_gpu_am_forward(ce_gpu_ctx *ctx, const ce_gpu_model *m, const ce_gpu_plan 
     int ldy = 0;
     const uint32_t *row_edge = p->d_row_edge.as<uint32_t>() + c.map_base;
     LatTail tail;
-    CE_TRY(run_steps(ctx, m, d_feats, m->input_dim, c.rows, row_src, row_edge, &y, &ldy, &tail));
+    CE_TRY(run_steps(ctx, m, d_feats, m->input_dim, c.rows, row_src, row_edge, &y, &ldy,
+                     lat_tail_ok(d_loglik, m->log_prior.as<float>()) ? &tail : nullptr));
     ProfScope prof(ctx, CE_GPU_PROF_FINALIZE);
     CE_TRY(finalize_output(ctx, y, ldy, 0, c.rows, m->num_pdfs, m->final_log_softmax, m->log_prior.as<float>(),
                            row_dst, d_loglik, tail));
@@ -1624,7 +1635,8 @@ int ce_gpu_nnet_propagate(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *d
   const float *y = nullptr;
   int ldy = 0;
   LatTail tail;
-  CE_TRY(run_steps(ctx, m, d_in, ld_in, rows, nullptr, nullptr, &y, &ldy, &tail));
+  CE_TRY(run_steps(ctx, m, d_in, ld_in, rows, nullptr, nullptr, &y, &ldy,
+                   lat_tail_ok(d_out, m->log_prior.as<float>()) ? &tail : nullptr));
   ProfScope prof(ctx, CE_GPU_PROF_FINALIZE);
   return finalize_output(ctx, y, ldy, m->net_left, out_rows, m->num_pdfs, m->final_log_softmax,
                          subtract_prior ? m->log_prior.as<float>() : nullptr, nullptr, d_out, tail);
@@ -1682,7 +1694,8 @@ int ce_gpu_nnet_propagate_blocks(ce_gpu_ctx *ctx, const ce_gpu_model *m, const f
   // blocks are independent: the rows a Splice reads across a block boundary
   // only feed rows that block's Narrow drops
   LatTail tail;
-  CE_TRY(run_steps(ctx, m, d_in, ld_in, rows, nullptr, d_edge, &y, &ldy, &tail));
+  CE_TRY(run_steps(ctx, m, d_in, ld_in, rows, nullptr, d_edge, &y, &ldy,
+                   lat_tail_ok(d_out, m->log_prior.as<float>()) ? &tail : nullptr));
   ProfScope prof(ctx, CE_GPU_PROF_FINALIZE);
   return finalize_output(ctx, y, ldy, 0, rows, m->num_pdfs, m->final_log_softmax,
                          subtract_prior ? m->log_prior.as<float>() : nullptr, d_dst, d_out, tail);

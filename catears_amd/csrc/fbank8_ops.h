@@ -47,11 +47,14 @@ constexpr int kSamp = 25;    // sample pairs per lane (400 samples / 8 lanes / 2
 // (4 frames x 8 lanes) start 12 banks apart, so the post-pass power stores
 // (a frame's lanes 16 floats apart) land on 8 banks instead of 4: C2 exact
 // 1.018-1.022 -> 1.040-1.048 G frames/s against 264 (260: 1.005-1.013;
-// tools/experiments/gpu_r4e.sh).  Any value >= 260 gives the same bits.
+// tools/experiments/gpu_r4e.sh).  Any value >= 260 that is a multiple of 4
+// gives the same bits (load_b, store_b and mel_window use 16-byte LDS
+// accesses at region-relative offsets).
 #ifndef FB8_STRIDE
 #define FB8_STRIDE 268
 #endif
 constexpr int kStride = FB8_STRIDE;
+static_assert(kStride % 4 == 0 && kStride >= 260, "frame regions: 16-byte aligned, room for 257 bins + padding");
 constexpr int kOpsA = 23;    // phase-A node ops per lane
 constexpr int kTwA = 8;      // floats per phase-A twiddle record (6 used)
 

@@ -159,11 +159,13 @@ __device__ __forceinline__ float apply_post(float y, float sc, float of, const i
 // wrote just before, or overwrite what they just read.  The wave waits for
 // all of its LDS operations to complete (lgkmcnt(0)) before it issues the
 // next one; the "memory" clobber keeps the compiler from moving LDS accesses
-// across.  A wavefront-scope fence plus wave_barrier -- the rounds 1-4 form
-// -- emits no wait at all, so it relied on a wave's LDS operations taking
-// effect in issue order.  Under concurrent MFMA-heavy kernels on the same CU
-// that did not hold: reads by the last 16 lanes returned data from before
-// the preceding write (GPUTEST_r04).
+// across.  The rounds 1-4 form (a wavefront-scope fence plus wave_barrier)
+// emits no wait and relies on a wave's LDS operations taking effect in issue
+// order.  It was suspected for round 4's fast-fbank differences, but the
+// stress test cleared it (the cause was packed-FP32 VALU);
+// the explicit wait is kept because it costs nothing measurable (C2 exact
+// 1.66 -> 1.68 G frames/s, tools/experiments/gpu_r5a.sh) and does not depend
+// on that ordering.
 __device__ __forceinline__ void wave_lds_sync() {
 #if defined(__HIP_DEVICE_COMPILE__)
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -456,10 +458,6 @@ int gemm_k_align();
 // (y16, plane stride py) or fp32 (y32).
 int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a);
 constexpr int kX6DirUnits = 256;  // gemm_bf16x6d_kernel's unit tile
-// Latency mode (kernels/gemm_bf16x6_lat.hip): one launch per layer, 16-unit
-// tiles, K split over a block's four waves (a function of K only) and summed
-// in wave order in LDS, + bias / ReLU / BatchNorm; needs the weight fragment
-// image (a.wd) and fp32 activations (din a multiple of 8).
 // Latency mode (kernels/gemm_bf16x6_lat.hip): K split into
 // x6_lat_slices(kpad, n) slices (a function of K and N only), every slice's
 // fp32 partial stored, then summed in slice order by a reduce kernel that

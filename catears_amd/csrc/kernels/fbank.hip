@@ -40,7 +40,7 @@ constexpr int kFramesPerBlock = 4;  // granularity of the plan's block_utt table
 #define FBANK_WAVES 8
 #endif
 constexpr int kWaves = FBANK_WAVES;  // waves per block (8 frames each)
-constexpr int kBlocksPerCU = kWaves == 8 ? 2 : 3;  // LDS: kWaves x 8 x 1056 B of frame regions + 11.5 KB of tables
+constexpr int kBlocksPerCU = kWaves == 8 ? 2 : 3;  // LDS: kWaves x 8 x kStride x 4 B (1072 B) frames + the tables
 
 __device__ __forceinline__ void wave_sync() { wave_lds_sync(); }
 
@@ -69,6 +69,10 @@ __global__ __launch_bounds__(kWaves * 64, 4) void fbank_kernel(const FbankTables
                                                             float *__restrict__ feats, float *__restrict__ mel_out) {
   __shared__ __attribute__((aligned(16))) float lds[kWaves * kLanes * kStride];
   __shared__ __attribute__((aligned(16))) Fb8Lds T;
+  // kBlocksPerCU blocks must fit the CU's 160 KB of LDS, or occupancy drops
+  // silently (the launch bound would still allow them)
+  static_assert(kBlocksPerCU * (sizeof(float) * kWaves * kLanes * kStride + sizeof(Fb8Lds)) <= 160 * 1024,
+                "fbank_kernel: LDS for kBlocksPerCU blocks exceeds 160 KB");
   for (int i = threadIdx.x; i < kOpsA * kLanes * kTwA; i += kWaves * 64) T.twa[i] = tab->fb8_twa[i];
   for (int i = threadIdx.x; i < kWinLen; i += kWaves * 64) T.win[i] = tab->window[i];
   for (int i = threadIdx.x; i < 2 * 129; i += kWaves * 64) T.kn[i] = tab->kn[i];

@@ -1131,7 +1131,7 @@ int launch_d(hipStream_t s, X6Args p) {
   p.tiles_n = (p.n + C::BW - 1) / C::BW;
   p.tiles_m = (p.m + C::BF - 1) / C::BF;
   dim3 grid(p.tiles_m * p.tiles_n), block(C::NT);
-  if (p.row_map || (p.nseg > 1 && p.din % 32 != 0))
+  if (p.row_map || p.din % 32 != 0)  // the same rule as launch_gemm_bf16x6's `first`
     hipLaunchKernelGGL((gemm_bf16x6d_kernel<C, true>), grid, block, 0, s, p);
   else
     hipLaunchKernelGGL((gemm_bf16x6d_kernel<C>), grid, block, 0, s, p);

@@ -173,6 +173,37 @@ def test_first_layer_reads_stay_inside_the_input(torch, G, lctx, xs_config):
         assert np.array_equal(bits(got), bits(want))
 
 
+def test_unspliced_first_linear_reads_stay_inside_the_input(torch, G, lctx, oracle):
+    """A model whose first component is a Linear on the raw 40-wide rows (no
+    Splice): din 40 is not a whole K-tile, so both the throughput and the
+    latency kernels must gather it (the throughput kernel picked
+    the plain loader for nseg == 1 and read 24 floats past the caller's
+    last row).  Input at the very end of a 2 MiB allocation; same bits as
+    from an ordinary tensor in both modes, and the oracle's values."""
+    from catears_amd import formats, synth
+    layers, left, right, prior = synth.tdnn_layers(256, 512, seed=29)
+    rng = np.random.default_rng(31)
+    first = [{"kind": "linear", "W": (rng.uniform(-1, 1, (40, 40)) * np.sqrt(3.0 / 40)).astype(np.float32),
+              "b": (0.1 * rng.uniform(-1, 1, 40)).astype(np.float32)}, {"kind": "relu"}]
+    layers = first + layers
+    image = formats.nnet_bytes(layers, left, right)
+    tctx = G.Context(0)
+    rows = 70
+    n = 2 * 1024 * 1024 // 4
+    buf = torch.empty(n, dtype=torch.float32, device="cuda")
+    x = buf[n - rows * 40:].view(rows, 40)
+    host = np.random.default_rng(771).normal(0.0, 3.0, size=(rows, 40)).astype(np.float32)
+    x.copy_(torch.from_numpy(host))
+    ref = oracle.nnet_propagate(layers, host)
+    for c in (lctx, tctx):
+        m = G.Model(c, image=image, prior=prior)
+        got = G.nnet_propagate(c, m, x).cpu().numpy()
+        want = G.nnet_propagate(c, m, dev(torch, host)).cpu().numpy()
+        assert np.array_equal(bits(got), bits(want))
+        assert np.isfinite(got).all()
+        assert np.abs(got - ref).max() <= LOGLIK_TOL
+
+
 POST_CHILD = r"""
 import sys, numpy as np, torch
 sys.path.insert(0, sys.argv[2])
