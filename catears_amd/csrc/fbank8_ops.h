@@ -43,43 +43,56 @@ namespace fb8 {
 constexpr int kLanes = 8;    // lanes per frame
 constexpr int kPts = 32;     // complex points per lane
 constexpr int kSamp = 25;    // sample pairs per lane (400 samples / 8 lanes / 2)
-// Floats per frame in LDS: 256 points + 12.  The frames of a 32-lane group
-// (4 frames x 8 lanes) start 12 banks apart, so the post-pass power stores
-// (a frame's lanes 16 floats apart) land on 8 banks instead of 4: C2 exact
-// 1.018-1.022 -> 1.040-1.048 G frames/s against 264 (260: 1.005-1.013;
-// tools/experiments/gpu_r4e.sh).  Any value >= 260 that is a multiple of 4
-// gives the same bits (load_b, store_b and mel_window use 16-byte LDS
-// accesses at region-relative offsets).
+// Floats per frame in LDS: 256 points + 8 (the phase A -> B transpose puts
+// 4 floats of padding after point 127, tpos_a).  264 = 8 mod 32: the four
+// frames of a 32-lane group start 8 banks apart, so the phase-A stores (8
+// consecutive lanes of a frame) and the power-spectrum stores (8 lanes on 8
+// consecutive bins) of a group fill the 32 banks exactly once
+// (tools/fb_bank_model2.py).  Any value >= 260 that is a multiple of 4 gives
+// the same bits (load_b and mel_window use 16-byte LDS accesses at
+// region-relative offsets).
 #ifndef FB8_STRIDE
-#define FB8_STRIDE 268
+#define FB8_STRIDE 264
 #endif
 constexpr int kStride = FB8_STRIDE;
 static_assert(kStride % 4 == 0 && kStride >= 260, "frame regions: 16-byte aligned, room for 257 bins + padding");
 constexpr int kOpsA = 23;    // phase-A node ops per lane
 constexpr int kTwA = 8;      // floats per phase-A twiddle record (6 used)
 
-// LDS: point p of a frame at float p of the frame's region (no swizzle:
-// every LDS address of the lane program is then a per-lane base plus a
+// LDS: every address of the lane program is a per-lane base plus a
 // compile-time offset, so the frame loop keeps no per-access address
-// registers).  Bank spread comes from the lane -> point assignment instead:
-// phase-A stores of a frame's lanes are consecutive, and the post-pass slots
-// (post_k) put the eight lanes' bit-reversed reads on distinct banks.
+// registers.  Bank spread comes from the lane -> point assignment instead.
 
 // Phase-B blocks (16 points each) of lane q: the first is always an X block
 // (a length-16 node and its subtree), the second a Y block (two length-8
 // nodes) for q < 5 and an X block otherwise.  Of the 16 blocks, Y are
-// 1, 5, 7, 9, 13: the second halves of the five length-32 nodes.
-constexpr int kBlk1[kLanes] = {0, 2, 3, 4, 6, 8, 11, 14};
-constexpr int kBlk2[kLanes] = {1, 5, 7, 9, 13, 10, 12, 15};
+// 1, 5, 7, 9, 13: the second halves of the five length-32 nodes.  DIF block
+// b holds the natural FFT indices k = 16 m + brev4(b) (the points of a block
+// are one residue class r = brev4(b) mod 16), and the blocks are paired so
+// that lane q holds the classes r and 16 - r (lane 0: 0 and 8): both
+// operands of every real-FFT post-pass pair (k, 256 - k) then sit in the
+// lane's own registers, and the post-pass needs no LDS exchange at all.
+constexpr int kBlk1[kLanes] = {0, 4, 10, 6, 14, 8, 12, 2};
+constexpr int kBlk2[kLanes] = {1, 7, 13, 5, 9, 15, 11, 3};
+// the same tables as nibbles, for a run-time lane index (shift and mask
+// instead of an indexed load): kBlk1, kBlk2 and the class brev4(kBlk1[q])
+constexpr uint32_t kBlk1N = 0x2C8E6A40u, kBlk2N = 0x3BF95D71u, kClassN = 0x43176520u;
+CE_HD int nib(uint32_t v, int q) { return (int)((v >> (4 * q)) & 15u); }
 CE_HD bool second_is_x(int q) { return q >= 5; }
 
-// Mel slots: lane q forms band 8c + q in slot c over a window of kMelW[c]
-// bins starting at a multiple of 4 (weights zero outside the band, so the
-// sum is the reference's sequential dot: 0 * p adds +0).
+// Mel slots: lane q forms band mel_band(c, q) = 8c + perm_c(q) in slot c
+// over a window of kMelW[c] bins starting at a multiple of 4 (weights zero
+// outside the band, so the sum is the reference's sequential dot: 0 * p
+// adds +0).  The permutations put the eight lanes' window starts on banks
+// the four frames of a ds_read_b128 lane group share least: 92 extra passes
+// per 8-frame group instead of 170 with perm_c(q) = q
+// (tools/fb_bank_model2.py, exhaustive per slot).
 constexpr int kMelSlots = 5;
 constexpr int kMelW[kMelSlots] = {8, 12, 16, 24, 32};
 constexpr int kMelWBase[kMelSlots] = {0, 8, 20, 36, 60};
 constexpr int kMelWTot = 92;  // lane q's windows back to back at q * kMelWTot
+constexpr uint32_t kMelPermN[kMelSlots] = {0x76543210u, 0x54327610u, 0x76534210u, 0x75316420u, 0x75436210u};
+CE_HD int mel_band(int c, int q) { return 8 * c + (int)((kMelPermN[c] >> (4 * q)) & 15u); }
 
 // ----------------------------------------------------------- node ops --
 
@@ -283,15 +296,11 @@ CE_HD void phase_b(float *re, float *im, int q, const float *tw16) {
 }
 
 // point held in register j of lane q in phase B
-CE_HD int phase_b_point(int q, int j) { return 16 * (j < 16 ? kBlk1[q] : kBlk2[q]) + (j & 15); }
+CE_HD int phase_b_point(int q, int j) { return 16 * (j < 16 ? nib(kBlk1N, q) : nib(kBlk2N, q)) + (j & 15); }
 
 // ------------------------------------------------ real-FFT post + power --
 
-// k of lane q's post-pass slot t (t = 0..15): every k in 1..128 once.  For
-// t < 15, bitrev8(k) = bitrev4(t + 1) << 4 | bitrev3(q) << 1 and
-// bitrev8(256 - k) = 255 - (bitrev3(q) << 1) - (bitrev4(t) << 4): a lane base
-// plus a constant, and the eight lanes of a frame on eight banks.
-CE_HD int post_k(int q, int t) { return 1 + t + 16 * q; }
+CE_HD int brev4(int v) { return ((v & 1) << 3) | ((v & 2) << 1) | ((v >> 1) & 2) | ((v >> 3) & 1); }
 
 // power[k] and power[256 - k] from B_k = (xr, xi), B_{256-k} = (yr, yi)
 // (srfft.cc:394-438 then fbank.cc:201-208); the float halving is exact, as
@@ -311,6 +320,46 @@ CE_HD void post_pair(float xr, float xi, float yr, float yi, float kr, float ki,
   *pkk = p_re * p_re + p_im * p_im;
 }
 
+// The real-FFT post-pass and power spectrum of lane q's sixteen pairs, from
+// its phase-B registers (B_k of point p = 16 b + j in register j of its block)
+// into pw[0..256] (the frame's LDS region, reused).  Slot t = 0..15, c =
+// brev4(t):
+//   c <= 7: k = A + 16 c (A = r, lane 0: 8), B_k in register t (lane 0:
+//           16 + t), B_{256-k} in register 31 - t;
+//   c >= 8: k = (16 - r) + 16 (15 - c), B_k in register 31 - t (lane 0:
+//           brev4(16 - c)), B_{256-k} in register t.
+// So k runs over 1..128 once per frame (lane 0 takes the classes 8 and 0,
+// with k = 128 pairing with itself), always the reference's k <= 128 form
+// of the pair; every LDS address is a per-lane base plus a constant; for a
+// given slot the eight lanes store to eight consecutive bins.  The k = 128
+// pair's second value is stored first and then overwritten by the first, as
+// the reference's loop leaves it.  DC and Nyquist (B_0, lane 0) are the
+// caller's.
+CE_HD void post_regs(int q, const float *re, const float *im, const float *kn, float *pw) {
+  const bool z = q == 0;
+  const int r = nib(kClassN, q);
+  const int a = z ? 8 : r;
+  const float *ka = kn + 2 * a, *kc = kn + 2 * (16 - r);
+  float *pa = pw + a, *pak = pw + (256 - 112) - a, *pc = pw + (16 - r), *pd = pw + r;
+  CE_UNROLL
+  for (int t = 0; t < 16; ++t) {
+    const int c = brev4(t);
+    float pk, pkk;
+    if (c <= 7) {
+      const float xr = z ? re[16 + t] : re[t], xi = z ? im[16 + t] : im[t];
+      post_pair(xr, xi, re[31 - t], im[31 - t], ka[32 * c], ka[32 * c + 1], &pk, &pkk);
+      pak[112 - 16 * c] = pkk;  // pw[256 - k]
+      pa[16 * c] = pk;          // pw[k]
+    } else {
+      const int j0 = brev4((16 - c) & 15);
+      const float xr = z ? re[j0] : re[31 - t], xi = z ? im[j0] : im[31 - t];
+      post_pair(xr, xi, re[t], im[t], kc[32 * (15 - c)], kc[32 * (15 - c) + 1], &pk, &pkk);
+      pd[16 * c] = pkk;         // pw[256 - k]
+      pc[16 * (15 - c)] = pk;   // pw[k]
+    }
+    if (t % 4 == 3) CE_SCHED_FENCE();
+  }
+}
 
 // ------------------------------------------------ samples, DC, window --
 
@@ -351,21 +400,16 @@ CE_HD void lane_window(const Sample *src, float mean, int r, const float *win, f
 
 // ------------------------------------------------------- LDS exchanges --
 
-// LDS position of FFT point p during the phase B -> post-pass transpose:
-// four floats of padding after every 64 points.  The sixteen 16-point
-// blocks then start on sixteen distinct 4-bank groups, so a frame's eight
-// lanes writing one block each (store_b) never share a bank (without it the
-// blocks started on 4 bank groups: 3-way conflicts).  Points 0..255 ->
-// 0..267: the 268-float frame.  The phase A -> B transpose keeps the plain
-// positions: with the guide's lane groups for ds_read_b128 its load_b
-// conflicts less that way (tools/fb_bank_model.py: 96 vs 160 extra passes
-// per group).  Every access below stays a lane base plus an immediate.
-CE_HD constexpr int tpos(int p) { return p + 4 * (p >> 6); }
+// LDS position of FFT point p during the phase A -> B transpose: four
+// floats of padding after point 127.  With the 264-float frame stride this
+// gives the load_b reads 64 extra passes per 8-frame group instead of 96
+// (tools/fb_bank_model2.py).  Points 0..255 -> 0..259.
+CE_HD constexpr int tpos_a(int p) { return p + 4 * (p >> 7); }
 
 // phase A -> LDS: lane r's point r + 8j from register j
 CE_HD void store_a(const float *v, int r, float *fbuf) {
   CE_UNROLL
-  for (int j = 0; j < kPts; ++j) fbuf[r + 8 * j] = v[j];
+  for (int j = 0; j < kPts; ++j) fbuf[r + 8 * j + (j >= 16 ? 4 : 0)] = v[j];
 }
 
 // four floats at a 16-byte aligned LDS address (one ds_read/write_b128)
@@ -373,54 +417,15 @@ struct alignas(16) F4 {
   float x, y, z, w;
 };
 
-// LDS <-> phase B registers: whole aligned groups of four points 
+// LDS -> phase B registers: whole aligned groups of four points, block
+// bases per lane (tpos_a's padding is a constant per block)
 CE_HD void load_b(int q, const float *fbuf, float *v) {
+  const int b1 = nib(kBlk1N, q), b2 = nib(kBlk2N, q);
+  const float *s1 = fbuf + tpos_a(16 * b1), *s2 = fbuf + tpos_a(16 * b2);
   CE_UNROLL
   for (int j = 0; j < kPts; j += 4) {
-    const F4 t = *reinterpret_cast<const F4 *>(fbuf + phase_b_point(q, j));
+    const F4 t = *reinterpret_cast<const F4 *>((j < 16 ? s1 : s2) + (j & 15));
     v[j] = t.x, v[j + 1] = t.y, v[j + 2] = t.z, v[j + 3] = t.w;
-  }
-}
-CE_HD void store_b(int q, const float *v, float *fbuf) {
-  CE_UNROLL
-  for (int j = 0; j < kPts; j += 4)
-    *reinterpret_cast<F4 *>(fbuf + tpos(phase_b_point(q, j))) = F4{v[j], v[j + 1], v[j + 2], v[j + 3]};
-}
-
-// the post-pass operands of lane q's slots: B_k and B_{256-k} (bit-reversed
-// positions: the DIF output before srfft.cc's BitReversePermute)
-CE_HD int brev3(int v) { return ((v & 1) << 2) | (v & 2) | ((v >> 2) & 1); }
-CE_HD int brev4(int v) { return ((v & 1) << 3) | ((v & 2) << 1) | ((v >> 1) & 2) | ((v >> 3) & 1); }
-CE_HD void load_post(int q, const float *fbuf, float *x, float *y) {
-  // bitrev8(post_k(q, t)) and bitrev8(256 - post_k(q, t)) as a lane base and
-  // a constant (post_k); slot 15 (k = 16 (q + 1)) from its own lane terms
-  // (offsets non-negative: an LDS instruction's offset field is unsigned)
-  // (the tpos padding of those points is a constant per t: 2 brev3(q) < 16
-  // never carries across a 64-point boundary)
-  const float *bx = fbuf + (brev3(q) << 1), *by = fbuf + 15 - (brev3(q) << 1);
-  CE_UNROLL
-  for (int t = 0; t < 15; ++t) {
-    x[t] = bx[tpos(brev4(t + 1) << 4)];
-    y[t] = by[tpos(255 - (brev4(t) << 4)) - 15];
-  }
-  x[15] = fbuf[brev4(q + 1)];
-  y[15] = fbuf[brev4(15 - q)];
-}
-
-// power spectrum of lane q's slots into pw[0..256] (k = 128 pairs with
-// itself: its second value is written first and then overwritten)
-CE_HD void post_store(int q, const float *xr, const float *xi, const float *yr, const float *yi, const float *kn,
-                      float *pw) {
-  // pw[k] = pw[16q + 1 + t], pw[256 - k] = pw[(240 - 16q) + 15 - t]
-  float *p0 = pw + 16 * q + 1, *p1 = pw + 240 - 16 * q;
-  const float *kq = kn + 2 * post_k(q, 0);
-  CE_UNROLL
-  for (int t = 0; t < 16; ++t) {
-    float pk, pkk;
-    post_pair(xr[t], xi[t], yr[t], yi[t], kq[2 * t], kq[2 * t + 1], &pk, &pkk);
-    p1[15 - t] = pkk;
-    p0[t] = pk;
-    if (t % 4 == 3) CE_SCHED_FENCE();
   }
 }
 

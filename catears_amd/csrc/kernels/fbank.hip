@@ -15,8 +15,9 @@
 //      the lane's residue class mod 8, in registers;
 //   4. one transpose through the wave's LDS (re, then im), then phase B: the
 //      length-16/8/4/2 nodes of the lane's two 16-point blocks, in registers;
-//   5. the FFT output back to LDS; the real-FFT post-pass + power spectrum
-//      for 16 k per lane (bit-reversed reads), power into LDS;
+//   5. the real-FFT post-pass + power spectrum for the lane's 16 pairs (k,
+//      256 - k), both operands in its own registers (its blocks are the
+//      residue classes r and 16 - r), power into LDS;
 //   6. five mel bands per lane over zero-padded 4-aligned windows (16-byte
 //      LDS reads), floor at FLT_EPSILON, logf, store.
 // Every float operation up to the final logf is the reference's, in the
@@ -124,24 +125,13 @@ __global__ __launch_bounds__(kWaves * 64, 4) void fbank_kernel(const FbankTables
     wave_sync();
     load_b(r, fbuf, im);
     phase_b(re, im, r, tw16);
-    wave_sync();
-    // 5. real-FFT post-pass + power spectrum
-    float xr[16], yr[16], xi[16], yi[16];
+    wave_sync();  // every lane's load_b reads are done: the region takes the power spectrum
+    // 5. real-FFT post-pass + power spectrum, operands from the lane's own
+    // registers (fbank8_ops.h post_regs)
     __builtin_amdgcn_sched_barrier(0);
-    store_b(r, re, fbuf);
-    wave_sync();
-    load_post(r, fbuf, xr, yr);
-    const float e0r = fbuf[0];
-    wave_sync();
-    store_b(r, im, fbuf);
-    wave_sync();
-    load_post(r, fbuf, xi, yi);
-    const float e0i = fbuf[0];
-    wave_sync();
-    __builtin_amdgcn_sched_barrier(0);
-    post_store(r, xr, xi, yr, yi, T.kn, fbuf);
-    if (r == 0) {  // DC and Nyquist bins (srfft.cc:446-451, fbank.cc:203-204)
-      const float z = e0r + e0i, nyq = e0r - e0i;
+    post_regs(r, re, im, T.kn, fbuf);
+    if (r == 0) {  // DC and Nyquist bins from B_0 (srfft.cc:446-451, fbank.cc:203-204)
+      const float z = re[0] + im[0], nyq = re[0] - im[0];
       fbuf[0] = z * z;
       fbuf[256] = nyq * nyq;
     }
@@ -162,7 +152,7 @@ __global__ __launch_bounds__(kWaves * 64, 4) void fbank_kernel(const FbankTables
     // costs ~70 registers here, the compiler's choice)
 #pragma unroll
     for (int c = 0; c < kMelSlots; ++c) {
-      const int b = 8 * c + r;
+      const int b = mel_band(c, r);
       if (MEL) mel_out[fc * kMel + b] = e[c];
       feats[fc * kMel + b] = logf(e[c] < FLT_EPSILON ? FLT_EPSILON : e[c]);
     }

@@ -659,8 +659,15 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
 //   WAR: activation stage (kt+1) % 2 was last read in tile kt-1, before the
 //        barrier that closed it; RAW: its writes precede the barrier that
 //        closes tile kt.
-template <class C, bool FIRST = false>
+// DIAG (ablation builds, wrong results, timing only; -DCATEARS_DIAG): bit 1 =
+// no split (the fp32 bits written as the planes), 2 = no activation stage
+// writes at all, 4 = no activation loads after the prologue, 8 = no weight
+// loads after the prologue, 16 = no K-tile barrier, 32 = no MFMAs.
+template <class C, bool FIRST = false, int DIAG = 0>
 __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
+#ifndef CATEARS_DIAG
+  static_assert(DIAG == 0, "ablation builds (wrong results) only with -DCATEARS_DIAG");
+#endif
   constexpr int BF = C::BF, TW = C::TW, TF = C::TF, NT = C::NT;
   constexpr int RPP = NT / 4;  // activation rows per pass (4 threads x 32 B per row)
   static_assert(BF == RPP, "one activation row chunk per thread");
@@ -686,6 +693,9 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
   for (int i = 0; i < TW; ++i)
     wb[i] = (gfrag *)(p.wd + ((size_t)((n0 >> 4) + ww * TW + i) * p.wd_kt * 3 * 64 + lane) * 8);
   auto load_w = [&](int kt, int pl, bf16x8 *dst) {
+    if constexpr ((DIAG & 8) != 0) {
+      if (kt > 0) return;
+    }
     kt = min(kt, ktiles - 1);
 #pragma unroll
     for (int i = 0; i < TW; ++i) dst[i] = wb[i][(kt * 3 + pl) * 64];
@@ -705,6 +715,9 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
     __syncthreads();
   }
   auto load_x = [&](int kt, int r) {
+    if constexpr ((DIAG & 4) != 0) {
+      if (kt > 1) return;
+    }
     kt = min(kt, ktiles - 1);
     const int k0 = kt * 32;
     if constexpr (FIRST) {
@@ -728,8 +741,19 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
     }
   };
   auto put = [&](char *st, int r) {
-    const Planes2 q0 = split3_pair(rx0[r].x, rx0[r].y), q1 = split3_pair(rx0[r].z, rx0[r].w);
-    const Planes2 q2 = split3_pair(rx1[r].x, rx1[r].y), q3 = split3_pair(rx1[r].z, rx1[r].w);
+    if constexpr ((DIAG & 2) != 0) return;
+    Planes2 q0, q1, q2, q3;
+    if constexpr ((DIAG & 1) != 0) {
+      auto raw = [](float a, float b) {
+        const uint32_t u = __builtin_bit_cast(uint32_t, a) ^ __builtin_bit_cast(uint32_t, b);
+        return Planes2{u, u >> 1, u >> 2};
+      };
+      q0 = raw(rx0[r].x, rx0[r].y), q1 = raw(rx0[r].z, rx0[r].w);
+      q2 = raw(rx1[r].x, rx1[r].y), q3 = raw(rx1[r].z, rx1[r].w);
+    } else {
+      q0 = split3_pair(rx0[r].x, rx0[r].y), q1 = split3_pair(rx0[r].z, rx0[r].w);
+      q2 = split3_pair(rx1[r].x, rx1[r].y), q3 = split3_pair(rx1[r].z, rx1[r].w);
+    }
     const int off = prow * 64 + ((pch ^ swz(prow)) * 16);
     *reinterpret_cast<u32x4 *>(st + off) = u32x4{q0.h, q1.h, q2.h, q3.h};
     *reinterpret_cast<u32x4 *>(st + BF * 64 + off) = u32x4{q0.m, q1.m, q2.m, q3.m};
@@ -773,37 +797,48 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
     read_b(st, 1, b1);
     load_w(kt + 1, 0, a0[c ^ 1]);
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr ((DIAG & 32) == 0) {
 #pragma unroll
-    for (int i = 0; i < TW; ++i)
+      for (int i = 0; i < TW; ++i)
 #pragma unroll
-      for (int j = 0; j < TF; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[c][i], b0[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TF; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[c][i], b0[j], acc[i][j], 0, 0, 0);
+    }
     __builtin_amdgcn_sched_barrier(0);
     load_x(kt + 2, c);
     __builtin_amdgcn_sched_barrier(0);
     put(sn, c ^ 1);
+    if constexpr ((DIAG & 32) == 0) {
 #pragma unroll
-    for (int i = 0; i < TW; ++i)
+      for (int i = 0; i < TW; ++i)
 #pragma unroll
-      for (int j = 0; j < TF; ++j) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[c][i], b1[j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b0[j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b1[j], acc[i][j], 0, 0, 0);
-      }
+        for (int j = 0; j < TF; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[c][i], b1[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b0[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b1[j], acc[i][j], 0, 0, 0);
+        }
+    }
     read_b(st, 2, b2);
     __builtin_amdgcn_sched_barrier(0);
     load_w(kt + 1, 1, a1);
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr ((DIAG & 32) == 0) {
 #pragma unroll
-    for (int i = 0; i < TW; ++i)
+      for (int i = 0; i < TW; ++i)
 #pragma unroll
-      for (int j = 0; j < TF; ++j) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[c][i], b2[j], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2[i], b0[j], acc[i][j], 0, 0, 0);
-      }
+        for (int j = 0; j < TF; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[c][i], b2[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2[i], b0[j], acc[i][j], 0, 0, 0);
+        }
+    } else {
+      // keep the fragment registers live
+#pragma unroll
+      for (int j = 0; j < TF; ++j) acc[0][j][0] += (float)b0[j][0] + (float)b1[j][0] + (float)b2[j][0] +
+                                                   (float)a0[c][0][0] + (float)a1[0][0] + (float)a2[0][0];
+    }
     __builtin_amdgcn_sched_barrier(0);
     load_w(kt + 1, 2, a2);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if constexpr ((DIAG & 16) == 0) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
   int kt = 0;
@@ -1126,7 +1161,7 @@ int launch_r(hipStream_t s, X6Args p) {
 }
 #endif
 
-template <class C>
+template <class C, int DIAG = 0>
 int launch_d(hipStream_t s, X6Args p) {
   p.tiles_n = (p.n + C::BW - 1) / C::BW;
   p.tiles_m = (p.m + C::BF - 1) / C::BF;
@@ -1134,7 +1169,7 @@ int launch_d(hipStream_t s, X6Args p) {
   if (p.row_map || p.din % 32 != 0)  // the same rule as launch_gemm_bf16x6's `first`
     hipLaunchKernelGGL((gemm_bf16x6d_kernel<C, true>), grid, block, 0, s, p);
   else
-    hipLaunchKernelGGL((gemm_bf16x6d_kernel<C>), grid, block, 0, s, p);
+    hipLaunchKernelGGL((gemm_bf16x6d_kernel<C, false, DIAG>), grid, block, 0, s, p);
   CE_HIP(hipGetLastError());
   return CE_GPU_OK;
 }
@@ -1189,7 +1224,7 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
   if (a.kpad % 32 != 0 || a.din % (first ? 8 : 32) != 0 || a.din <= 0 || a.nseg < 1 || a.nseg > 8 ||
       a.nseg * a.din > a.kpad)
     return fail(CE_GPU_EINVAL, "gemm_bf16x6: bad K geometry");
-  if (first && (!a.xf || !a.wd || (x6_variant() != 0 && x6_variant() != 300)))
+  if (first && (!a.xf || !a.wd || (x6_variant() != 0 && x6_variant() != 300 && (x6_variant() < 310 || x6_variant() > 316))))
     return fail(CE_GPU_EINVAL, "gemm_bf16x6: a gathered first layer needs fp32 input and the direct-weight kernel");
   if (a.n % 4 != 0 || a.ldy % 4 != 0 || (a.y16 && a.py % 4 != 0))
     return fail(CE_GPU_EINVAL, "gemm_bf16x6: output width must be a multiple of 4");
@@ -1293,6 +1328,30 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
         return launch_ws<X6Cfg<128, 256, 2, 4, 2>, 4>(s, p);
 #endif
 #ifdef CATEARS_DIAG
+      // ablations of the direct-weight default 300 (layers 2-7; wrong results,
+      // timing only): 310 no split, 311 no activation stage writes, 312 no
+      // activation path, 313 no weight loads, 314 no barrier, 315 no MFMAs,
+      // 316 MFMAs only
+      case 310:
+      case 311:
+      case 312:
+      case 313:
+      case 314:
+      case 315:
+      case 316: {
+        if (!a.wd) return fail(CE_GPU_EINVAL, "ablations of 300 need the weight fragment image");
+        using D = X6Cfg<kX6DirUnits, 128, 4, 2, 2>;
+        if (first) return launch_d<X6Cfg<128, 128, 2, 4, 2>>(s, p);
+        switch (x6_variant()) {
+          case 310: return launch_d<D, 1>(s, p);
+          case 311: return launch_d<D, 2>(s, p);
+          case 312: return launch_d<D, 6>(s, p);
+          case 313: return launch_d<D, 8>(s, p);
+          case 314: return launch_d<D, 16>(s, p);
+          case 315: return launch_d<D, 32>(s, p);
+          default: return launch_d<D, 2 | 4 | 8 | 16>(s, p);
+        }
+      }
       // ablations of 55 (wrong results: timing only)
       case 91:
         return launch_f<X6Cfg<128, 256, 2, 4, 2>, 6, 1>(s, p);

@@ -159,7 +159,7 @@ void build_fb8(FbankTables *t) {
   twid(4, 3, t->fb8_tw16 + 6);
   for (int c = 0; c < fb8::kMelSlots; ++c)
     for (int q = 0; q < fb8::kLanes; ++q) {
-      const int b = 8 * c + q, W = fb8::kMelW[c];
+      const int b = fb8::mel_band(c, q), W = fb8::kMelW[c];
       const int st = std::min(t->mel_off[b] & ~3, kHalf - W);
       if (t->mel_off[b] < st || t->mel_off[b] + t->mel_len[b] > st + W) abort();  // fixed geometry (src/fbank.h)
       t->fb8_mel_st[c * fb8::kLanes + q] = st;

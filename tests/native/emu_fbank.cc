@@ -47,18 +47,11 @@ extern "C" int emu_fbank(const float *wave, long n, float *mel, float *feats) {
     for (int r = 0; r < kLanes; ++r) store_a(im[r], r, lds);
     for (int q = 0; q < kLanes; ++q) load_b(q, lds, im[q]);
     for (int q = 0; q < kLanes; ++q) phase_b(re[q], im[q], q, tab.fb8_tw16);
-    // FFT output back to LDS; post-pass operands
-    float xr[kLanes][16], yr[kLanes][16], xi[kLanes][16], yi[kLanes][16], e0r = 0, e0i = 0;
-    for (int q = 0; q < kLanes; ++q) store_b(q, re[q], lds);
-    for (int q = 0; q < kLanes; ++q) load_post(q, lds, xr[q], yr[q]);
-    e0r = lds[0];
-    for (int q = 0; q < kLanes; ++q) store_b(q, im[q], lds);
-    for (int q = 0; q < kLanes; ++q) load_post(q, lds, xi[q], yi[q]);
-    e0i = lds[0];
-    // power spectrum (the LDS region again), DC / Nyquist by lane 0
-    for (int q = 0; q < kLanes; ++q) post_store(q, xr[q], xi[q], yr[q], yi[q], tab.kn, lds);
+    // post-pass + power spectrum from each lane's registers into the LDS
+    // region, DC / Nyquist by lane 0
+    for (int q = 0; q < kLanes; ++q) post_regs(q, re[q], im[q], tab.kn, lds);
     {
-      const float z = e0r + e0i, nyq = e0r - e0i;
+      const float z = re[0][0] + im[0][0], nyq = re[0][0] - im[0][0];
       lds[0] = z * z;
       lds[256] = nyq * nyq;
     }
@@ -72,7 +65,7 @@ extern "C" int emu_fbank(const float *wave, long n, float *mel, float *feats) {
       e[3] = mel_window<24>(w + q * kMelWTot + kMelWBase[3], lds + st[3 * kLanes]);
       e[4] = mel_window<32>(w + q * kMelWTot + kMelWBase[4], lds + st[4 * kLanes]);
       for (int c = 0; c < kMelSlots; ++c) {
-        const int b = 8 * c + q;
+        const int b = mel_band(c, q);
         mel[(long)f * kMel + b] = e[c];
         feats[(long)f * kMel + b] = logf(e[c] < FLT_EPSILON ? FLT_EPSILON : e[c]);
       }

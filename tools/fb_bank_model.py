@@ -5,7 +5,8 @@ groups over 64 banks, ds_write_b128 in eight 8-lane groups over 32 banks,
 b32 reads / writes in two 32-lane groups over 32 banks; equal addresses
 broadcast.  Prints the extra passes per 8-frame group for frame strides S
 and transpose layouts phys(p) = p + P * (p >> G), one layout for both
-transposes and then one per transpose.  python tools/fb_bank_model.py"""
+transposes and then one per transpose (the round-4 lane program; round 5's
+register post-pass: tools/fb_bank_model2.py).  python tools/fb_bank_model.py"""
 kBlk1=[0,2,3,4,6,8,11,14]; kBlk2=[1,5,7,9,13,10,12,15]
 def brev3(v): return ((v&1)<<2)|(v&2)|((v>>2)&1)
 def brev4(v): return ((v&1)<<3)|((v&2)<<1)|((v>>1)&2)|((v>>3)&1)
@@ -44,18 +45,6 @@ def model(S,P,Gs):
     t['load_post']=2*sum(cost([lp(l,tt,w) for l in L],'r32') for tt in range(16) for w in 'xy')
     t['post_store']=sum(cost([fb(l)+16*(l&7)+1+tt for l in L],'w32')+cost([fb(l)+240-16*(l&7)+15-tt for l in L],'w32') for tt in range(16))
     return t
-import sys
-res=[]
-for S in range(260,276,4):
-  for Gs in (4,5,6,7):
-    for P in (0,4,8):
-      if 255+P*(255>>Gs) >= S: continue
-      t=model(S,P,Gs); res.append((sum(t.values()),S,P,Gs,t))
-res.sort(key=lambda x:x[0])
-for r in res[:10]: print(r)
-print('current', [r for r in res if r[1]==268 and r[2]==4 and r[3]==6])
-print('r04a', [r for r in res if r[1]==264 and r[2]==0 and r[3]==6])
-
 def model2(S,L1,L2):
     fb=lambda l: (l>>3)*S
     L=range(64); t={}
@@ -71,17 +60,30 @@ def model2(S,L1,L2):
     t['load_post']=2*sum(cost([lp(l,tt,w) for l in L],'r32') for tt in range(16) for w in 'xy')
     t['post_store']=sum(cost([fb(l)+16*(l&7)+1+tt for l in L],'w32')+cost([fb(l)+240-16*(l&7)+15-tt for l in L],'w32') for tt in range(16))
     return t
-print('--- separate layouts')
-res=[]
-lays=[]
-for Gs in (4,5,6,7):
-  for P in (0,4,8,12):
-    lays.append((P,Gs,(lambda P,Gs: (lambda p: p+P*(p>>Gs)))(P,Gs)))
-for S in (264,268,272):
-  for P1,G1,f1 in lays:
-    if f1(255)>=S: continue
-    for P2,G2,f2 in lays:
-      if f2(255)>=S: continue
-      t=model2(S,f1,f2); res.append((sum(t.values()),S,(P1,G1),(P2,G2),t))
-res.sort(key=lambda x:x[0])
-for r in res[:8]: print(r)
+
+if __name__ == '__main__':
+    import sys
+    res=[]
+    for S in range(260,276,4):
+      for Gs in (4,5,6,7):
+        for P in (0,4,8):
+          if 255+P*(255>>Gs) >= S: continue
+          t=model(S,P,Gs); res.append((sum(t.values()),S,P,Gs,t))
+    res.sort(key=lambda x:x[0])
+    for r in res[:10]: print(r)
+    print('current', [r for r in res if r[1]==268 and r[2]==4 and r[3]==6])
+    print('r04a', [r for r in res if r[1]==264 and r[2]==0 and r[3]==6])
+    print('--- separate layouts')
+    res=[]
+    lays=[]
+    for Gs in (4,5,6,7):
+      for P in (0,4,8,12):
+        lays.append((P,Gs,(lambda P,Gs: (lambda p: p+P*(p>>Gs)))(P,Gs)))
+    for S in (264,268,272):
+      for P1,G1,f1 in lays:
+        if f1(255)>=S: continue
+        for P2,G2,f2 in lays:
+          if f2(255)>=S: continue
+          t=model2(S,f1,f2); res.append((sum(t.values()),S,(P1,G1),(P2,G2),t))
+    res.sort(key=lambda x:x[0])
+    for r in res[:8]: print(r)
