@@ -681,7 +681,7 @@ def main_c4(args):
     if not args.no_profile:
         gpu.profile_anchor(local, backs[0])
         for c in set(ctxs + [ctx_f]):
-            c.profile(True, classes=[ctxs[0].PROF_GEMM])
+            c.profile(True, classes=None if args.stage_profile else [ctxs[0].PROF_GEMM])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -709,10 +709,31 @@ def main_c4(args):
     rows_in = gat.rows_in if gat is not None else 0
     busy = None
     n_gemm = 0
+    stages = None
     if not args.no_profile:
         iv = []
         for c in ctxs:
             iv += c.profile_intervals(c.PROF_GEMM)
+        if args.stage_profile:
+            # the front stream's share: fbank and CMVN run there, beside the
+            # nnet streams' GEMMs; a stage only holds the pipeline back when
+            # the front stream is busy most of the wall time
+            stages = {}
+            front = []
+            for name, cs, cls in (("fbank", [ctx_f], ctx_f.PROF_FBANK), ("cmvn", [ctx_f], ctx_f.PROF_CMVN),
+                                  ("finalize", ctxs, ctx_f.PROF_FINALIZE)):
+                civ = [x for c in cs for x in c.profile_intervals(cls)]
+                if cs == [ctx_f]:
+                    front += civ
+                if civ:
+                    u = gpu.union_ms(civ)
+                    stages[name] = {"launches": len(civ), "avg_ms": round(sum(b - a for a, b in civ) / len(civ), 4),
+                                    "busy_ms": round(u, 3), "share_of_wall": round(u / (elapsed * 1e3), 4)}
+            fu = gpu.union_ms(front) if front else 0.0
+            stages["front_stream"] = {"busy_ms": round(fu, 3), "share_of_wall": round(fu / (elapsed * 1e3), 4)}
+            if "cmvn" in stages and fu > 0:
+                stages["cmvn"]["share_of_front_busy"] = round(stages["cmvn"]["busy_ms"] / fu, 4)
+        for c in ctxs:
             c.profile(False)
         ctx_f.profile(False)
         n_gemm = len(iv)
@@ -754,6 +775,8 @@ def main_c4(args):
         "roofline": roofline, "cpu_baseline": None,
         "checksum": float(checksum.item()),
     }
+    if stages is not None:
+        line["stages"] = stages
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

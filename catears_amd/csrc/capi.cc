@@ -1402,17 +1402,6 @@ static int run_steps_x3(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, 
 
 // The int8 program (kernels/nnet_i8.hip): per Linear layer min/max ->
 // quantize (+ row sums) -> u8 GEMM with float epilogue.
-// CATEARS_I8_QFOLD=0: the round-4 form (a one-block params kernel, then the
-// quantize kernel); default 1: one launch that folds and quantizes (the same
-// bytes, row sums and parameters; tests/test_gpu_int8.py)
-static int i8_quant_fold() {
-  static const int v = [] {
-    const char *e = getenv("CATEARS_I8_QFOLD");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
-
 static int run_steps_i8(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, int ldx, int rows,
                         const int *row_map, const uint32_t *row_edge, const float **y, int *ldy) {
   const size_t per = (size_t)rows * m->max_width;
@@ -1447,23 +1436,12 @@ static int run_steps_i8(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, 
         const int zero[1] = {0};
         const int nseg = L.spliced ? st.gemm.nseg : 1;
         const int *offs = L.spliced ? st.gemm.off : zero;
-        if (i8_quant_fold()) {
-          // the (min, max) partials: from the previous GEMM's epilogue, or a
-          // minmax pass over this layer's input; folded inside the quantize
-          int nparts = fused_parts;
-          if (nparts == 0)
-            CE_TRY(launch_i8_minmax(ctx->stream, x, ldx, rows, L.in_width, rm, row_edge, L.in_left, L.in_right,
-                                    part, &nparts));
-          CE_TRY(launch_i8_quantize_fold(ctx->stream, x, ldx, rows, L.in_width, rm, nseg, offs, part, nparts,
-                                         params, xq, ldq, rowsum));
-        } else {
-          if (fused_parts > 0)
-            CE_TRY(launch_i8_params_fold(ctx->stream, part, fused_parts, params));
-          else
-            CE_TRY(launch_i8_params(ctx->stream, x, ldx, rows, L.in_width, rm, row_edge, L.in_left, L.in_right,
-                                    part, params));
-          CE_TRY(launch_i8_quantize(ctx->stream, x, ldx, rows, L.in_width, rm, nseg, offs, params, xq, ldq, rowsum));
-        }
+        if (fused_parts > 0)
+          CE_TRY(launch_i8_params_fold(ctx->stream, part, fused_parts, params));
+        else
+          CE_TRY(launch_i8_params(ctx->stream, x, ldx, rows, L.in_width, rm, row_edge, L.in_left, L.in_right,
+                                  part, params));
+        CE_TRY(launch_i8_quantize(ctx->stream, x, ldx, rows, L.in_width, rm, nseg, offs, params, xq, ldq, rowsum));
       }
       // the next step reads this GEMM's output directly: its min / max is
       // reduced in this GEMM's epilogue (the partials are read by the next

@@ -552,16 +552,6 @@ struct I8NextMinMax {
 int launch_i8_gemm(hipStream_t s, const I8Layer &L, const int8_t *a, int lda, int m, const int32_t *rowsum,
                    const void *pa, float *y, int ldy, const I8NextMinMax *mm = nullptr, int *nparts = nullptr);
 int launch_i8_params_fold(hipStream_t s, const void *part, int nparts, void *params);
-// minmax_kernel alone (its partials, *nparts of them, for launch_i8_quantize_fold)
-int launch_i8_minmax(hipStream_t s, const float *x, int ldx, int rows, int width, const int *row_map,
-                     const uint32_t *row_edge, int in_left, int in_right, void *part, int *nparts);
-// params fold + Quantize in one launch: every block folds the nparts (min,
-// max) partials into the layer's parameters (block 0 stores them to
-// `params` for the GEMM), then quantizes rows grid-stride; same bytes and
-// row sums as launch_i8_params_fold + launch_i8_quantize
-int launch_i8_quantize_fold(hipStream_t s, const float *x, int ldx, int rows, int width, const int *row_map,
-                            int nseg, const int *offs, const void *part, int nparts, void *params, int8_t *q,
-                            int ldq, int32_t *rowsum);
 size_t i8_gemm_parts(int m, int n);
 int i8_k_align();
 int launch_gemm_u8_ws(hipStream_t s, int m, int n, int k, const uint8_t *a, const void *pa,

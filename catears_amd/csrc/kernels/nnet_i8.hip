@@ -219,51 +219,6 @@ __global__ __launch_bounds__(256) void quantize_kernel(const float *__restrict__
   quantize_row(x, ldx, rows, width, row_map, nseg, so, p.scale, (float)p.zp, q, ldq, rowsum, r, lane);
 }
 
-// params_kernel + quantize_kernel in one launch: every block folds the
-// (min, max) partials itself (the same min / max, so the same parameters in
-// every block; block 0 also stores them for the GEMM epilogue), then its
-// waves quantize rows grid-stride.  One launch and one dependent hop per
-// layer fewer than the two kernels.
-constexpr int kQuantFoldBlocks = 512;
-
-__global__ __launch_bounds__(256) void quantize_fold_kernel(const float *__restrict__ x, int ldx, int rows, int width,
-                                                            const int *__restrict__ row_map, int nseg,
-                                                            SpliceOffsets so, const float2 *__restrict__ part,
-                                                            int nparts, QP *__restrict__ params_out,
-                                                            int8_t *__restrict__ q, int ldq,
-                                                            int32_t *__restrict__ rowsum) {
-  __shared__ float2 wv[4];
-  __shared__ QP sp;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float mn = FLT_MAX, mx = FLT_MIN;
-  for (int i = threadIdx.x; i < nparts; i += 256) {
-    const float2 v = part[i];
-    mn = v.x < mn ? v.x : mn;
-    mx = v.y > mx ? v.y : mx;
-  }
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    const float omn = __shfl_xor(mn, d, 64), omx = __shfl_xor(mx, d, 64);
-    mn = omn < mn ? omn : mn;
-    mx = omx > mx ? omx : mx;
-  }
-  if (lane == 0) wv[wave] = make_float2(mn, mx);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int w = 1; w < 4; ++w) {
-      mn = wv[w].x < mn ? wv[w].x : mn;
-      mx = wv[w].y > mx ? wv[w].y : mx;
-    }
-    sp = qparams(mn, mx);
-    if (blockIdx.x == 0) *params_out = sp;
-  }
-  __syncthreads();
-  const QP p = sp;
-  const float zp = (float)p.zp;
-  for (int r = blockIdx.x * 4 + wave; r < rows; r += gridDim.x * 4)
-    quantize_row(x, ldx, rows, width, row_map, nseg, so, p.scale, zp, q, ldq, rowsum, r, lane);
-}
-
 constexpr int IBM = 128, IBN = 128, IBK = 64, ILD = IBK + 16;  // bytes
 
 struct I8Args {
@@ -285,7 +240,6 @@ struct I8Args {
   int ldy;
   int tiles_n, tiles_m, group;
   int vec_epi;              // i8_epilogue_v (16-byte row stores)
-  int nt_store;             // ... non-temporal (CATEARS_I8_NT, default 1)
   // Non-null: the epilogue also reduces the (min, max) of its outputs over the
   // rows the NEXT layer's Quantize reads (minmax_kernel's held-row rule with
   // that layer's in_left / in_right) into mm_part[blockIdx.x], so the next
@@ -490,11 +444,8 @@ __device__ __forceinline__ void i8_epilogue_v(const I8Args &p, const i32x16 (&ac
         // tools/experiments/i8_nt.sh)
         if (row < p.m && col < p.n) {
           typedef float nt4 __attribute__((ext_vector_type(4)));
-          if (p.nt_store)
-            __builtin_nontemporal_store(nt4{v.x, v.y, v.z, v.w},
-                                        reinterpret_cast<nt4 *>(p.y + (int64_t)row * p.ldy + col));
-          else
-            *reinterpret_cast<nt4 *>(p.y + (int64_t)row * p.ldy + col) = nt4{v.x, v.y, v.z, v.w};
+          __builtin_nontemporal_store(nt4{v.x, v.y, v.z, v.w},
+                                      reinterpret_cast<nt4 *>(p.y + (int64_t)row * p.ldy + col));
         }
       }
       wave_lds_sync();
@@ -1108,28 +1059,6 @@ int launch_i8_quantize(hipStream_t s, const float *x, int ldx, int rows, int wid
   return CE_GPU_OK;
 }
 
-int launch_i8_quantize_fold(hipStream_t s, const float *x, int ldx, int rows, int width, const int *row_map,
-                            int nseg, const int *offs, const void *part, int nparts, void *params, int8_t *q,
-                            int ldq, int32_t *rowsum) {
-  SpliceOffsets so = {};
-  for (int i = 0; i < nseg; ++i) so.off[i] = offs[i];
-  const int blocks = std::max(1, std::min(kQuantFoldBlocks, (rows + 3) / 4));
-  hipLaunchKernelGGL(quantize_fold_kernel, dim3(blocks), dim3(256), 0, s, x, ldx, rows, width, row_map, nseg, so,
-                     static_cast<const float2 *>(part), nparts, static_cast<QP *>(params), q, ldq, rowsum);
-  CE_HIP(hipGetLastError());
-  return CE_GPU_OK;
-}
-
-int launch_i8_minmax(hipStream_t s, const float *x, int ldx, int rows, int width, const int *row_map,
-                     const uint32_t *row_edge, int in_left, int in_right, void *part, int *nparts) {
-  const int blocks = std::max(1, std::min(kMinmaxBlocks, (rows + 3) / 4));
-  hipLaunchKernelGGL(minmax_kernel, dim3(blocks), dim3(256), 0, s, x, ldx, rows, width, row_map, row_edge, in_left,
-                     in_right, static_cast<float2 *>(part));
-  CE_HIP(hipGetLastError());
-  *nparts = blocks;
-  return CE_GPU_OK;
-}
-
 int launch_i8_params_fold(hipStream_t s, const void *part, int nparts, void *params) {
   hipLaunchKernelGGL(params_kernel, dim3(1), dim3(256), 0, s, static_cast<const float2 *>(part), nparts,
                      static_cast<QP *>(params));
@@ -1174,11 +1103,7 @@ int launch_i8_gemm(hipStream_t s, const I8Layer &L, const int8_t *a, int lda, in
     return e ? atoi(e) : 1;
   }();
   p.vec_epi = vec_epi && L.n % 4 == 0 && ldy % 4 == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0;
-  static const int nt_store = [] {
-    const char *e = getenv("CATEARS_I8_NT");
-    return e ? atoi(e) : 1;
-  }();
-  p.nt_store = nt_store;
+
   static const int use_glds = [] {
     const char *e = getenv("CATEARS_I8_GEMM");
     return e ? atoi(e) : 16;  // measured best on TDNN-S, frame batch 8192 (tools/i8_sweep.sh)
