@@ -663,16 +663,26 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
 // no split (the fp32 bits written as the planes), 2 = no activation stage
 // writes at all, 4 = no activation loads after the prologue, 8 = no weight
 // loads after the prologue, 16 = no K-tile barrier, 32 = no MFMAs.
-template <class C, bool FIRST = false, int DIAG = 0>
+// KS: K-tiles per LDS stage.  KS = 2 holds two K-tiles per stage (96 KB for
+// both stages), so the block barrier comes once per two K-tiles; tile t
+// lives in sub-stage t & 1 of stage (t >> 1) & 1, tile t + 2 is split and
+// written during tile t and loaded during tile t - 1 (one tile more of load
+// slack).  Same products in the same order: bit-identical to KS = 1.
+template <class C, bool FIRST = false, int DIAG = 0, int KS = 1>
 __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
 #ifndef CATEARS_DIAG
   static_assert(DIAG == 0, "ablation builds (wrong results) only with -DCATEARS_DIAG");
 #endif
+  static_assert(KS == 1 || (KS == 2 && !FIRST), "two K-tiles per stage: hidden layers only (even K-tile count)");
   constexpr int BF = C::BF, TW = C::TW, TF = C::TF, NT = C::NT;
   constexpr int RPP = NT / 4;  // activation rows per pass (4 threads x 32 B per row)
   static_assert(BF == RPP, "one activation row chunk per thread");
   constexpr int ASTAGE = 3 * BF * 64;  // bytes: one K-tile of activation planes
-  __shared__ __attribute__((aligned(1024))) char smem[2 * ASTAGE];
+  __shared__ __attribute__((aligned(1024))) char smem[2 * KS * ASTAGE];
+  auto stage_of = [&](int t) -> char * {
+    if constexpr (KS == 1) return smem + (t & 1) * ASTAGE;
+    else return smem + ((((t >> 1) & 1) << 1) + (t & 1)) * ASTAGE;
+  };
   auto swz = [](int row) { return ((row >> 3) & 1) << 1; };
   typedef float f32x4v __attribute__((ext_vector_type(4)));
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -777,15 +787,22 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
   load_w(0, 0, a0[0]);
   load_w(0, 1, a1);
   load_w(0, 2, a2);
-  put(smem, 0);
-  load_x(1, 1);
+  if constexpr (KS == 1) {
+    put(smem, 0);
+    load_x(1, 1);
+  } else {
+    load_x(1, 1);
+    put(stage_of(0), 0);
+    put(stage_of(1), 1);
+    load_x(2, 0);
+  }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 
   auto body = [&](int kt, auto cc) {
     constexpr int c = decltype(cc)::value;
-    const char *st = smem + (kt & 1) * ASTAGE;
-    char *sn = smem + ((kt + 1) & 1) * ASTAGE;
+    const char *st = stage_of(kt);
+    char *sn = stage_of(kt + KS);
     // Regions (sched_barrier): the compiler would otherwise sink every load
     // to its registers' last use and then wait on it at the next tile's
     // head.  The loads sit in regions of their own at the top of the
@@ -804,9 +821,11 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
         for (int j = 0; j < TF; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[c][i], b0[j], acc[i][j], 0, 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
-    load_x(kt + 2, c);
+    // KS 1: load tile kt + 2 into rx[c], write tile kt + 1 from rx[c ^ 1];
+    // KS 2: load tile kt + 3 into rx[c ^ 1], write tile kt + 2 from rx[c]
+    load_x(kt + KS + 1, KS == 1 ? c : c ^ 1);
     __builtin_amdgcn_sched_barrier(0);
-    put(sn, c ^ 1);
+    put(sn, KS == 1 ? c ^ 1 : c);
     if constexpr ((DIAG & 32) == 0) {
 #pragma unroll
       for (int i = 0; i < TW; ++i)
@@ -837,8 +856,10 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
     }
     __builtin_amdgcn_sched_barrier(0);
     load_w(kt + 1, 2, a2);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if constexpr ((DIAG & 16) == 0) __builtin_amdgcn_s_barrier();
+    if constexpr (KS == 1 || c == 1) {  // KS 2: once per stage (after its odd tile)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if constexpr ((DIAG & 16) == 0) __builtin_amdgcn_s_barrier();
+    }
     __builtin_amdgcn_sched_barrier(0);
   };
   int kt = 0;
@@ -846,7 +867,7 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
     body(kt, std::integral_constant<int, 0>());
     body(kt + 1, std::integral_constant<int, 1>());
   }
-  if (kt < ktiles) body(kt, std::integral_constant<int, 0>());
+  if (KS == 1 && kt < ktiles) body(kt, std::integral_constant<int, 0>());
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail prefetches
   x6_epilogue<TW, TF, false>(p, acc, n0 + ww * TW * 16, f0 + frow, lane);
 }
@@ -1161,6 +1182,16 @@ int launch_r(hipStream_t s, X6Args p) {
 }
 #endif
 
+// CATEARS_X6_KS: K-tiles per LDS stage of the direct-weight kernel's hidden
+// layers (1 or 2; same bits)
+int x6_ks() {
+  static int v = [] {
+    const char *e = getenv("CATEARS_X6_KS");
+    return e ? atoi(e) : 2;
+  }();
+  return v;
+}
+
 template <class C, int DIAG = 0>
 int launch_d(hipStream_t s, X6Args p) {
   p.tiles_n = (p.n + C::BW - 1) / C::BW;
@@ -1168,6 +1199,8 @@ int launch_d(hipStream_t s, X6Args p) {
   dim3 grid(p.tiles_m * p.tiles_n), block(C::NT);
   if (p.row_map || p.din % 32 != 0)  // the same rule as launch_gemm_bf16x6's `first`
     hipLaunchKernelGGL((gemm_bf16x6d_kernel<C, true>), grid, block, 0, s, p);
+  else if (x6_ks() == 2 && (p.kpad / 32) % 2 == 0)
+    hipLaunchKernelGGL((gemm_bf16x6d_kernel<C, false, DIAG, 2>), grid, block, 0, s, p);
   else
     hipLaunchKernelGGL((gemm_bf16x6d_kernel<C, false, DIAG>), grid, block, 0, s, p);
   CE_HIP(hipGetLastError());

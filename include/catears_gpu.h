@@ -109,7 +109,8 @@ int ce_gpu_ctx_set_latency(ce_gpu_ctx *ctx, int on);
  *       (src/fbank.cc:44-245, src/srfft.cc:124-459): pre-log mel energies
  *       bit-identical to Fbank::Process, log-mel within 1e-5;
  *   CE_GPU_FBANK_FAST  a four-step 16 x 16 FFT with 16 lanes per frame and
- *       tabled twiddles, 1.3x the exact kernel's frame rate: log-mel within
+ *       tabled twiddles (since round 5 no faster than the exact kernel on
+ *       C2: 2.15 vs 2.2 G frames/s; kept as an option): log-mel within
  *       1e-4 of the reference on speech (and of its Kaldi dump), and as close
  *       to the exact float64 result as the reference's own fp32 order is
  *       (max 7.8e-5 vs the reference's 1.07e-4, p99.9 2.0e-5;
