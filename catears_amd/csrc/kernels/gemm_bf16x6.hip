@@ -1183,11 +1183,14 @@ int launch_r(hipStream_t s, X6Args p) {
 #endif
 
 // CATEARS_X6_KS: K-tiles per LDS stage of the direct-weight kernel's hidden
-// layers (1 or 2; same bits)
+// layers (1 or 2; same bits).  Measured (tools/experiments/gpu_r5e.sh, one
+// box, alternating): two per stage is 2 % slower -- serial hidden layer 158.5
+// vs 155.6 us, C3 at the driver's flags 6.36-6.38 vs 6.40-6.46 M frames/s --
+// so one stays the default; the barrier is not what the loop waits on.
 int x6_ks() {
   static int v = [] {
     const char *e = getenv("CATEARS_X6_KS");
-    return e ? atoi(e) : 2;
+    return e ? atoi(e) : 1;
   }();
   return v;
 }

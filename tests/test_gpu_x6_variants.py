@@ -55,9 +55,9 @@ def test_x6_variants_bit_identical(tmp_path, s_config):
     # the gathered first layer on the hidden layers' 256 x 128 tiles
     wide = _run(0, s_config, tmp_path / "t256.npy", CATEARS_X6_FIRST_TILE="256")
     assert np.array_equal(wide, base), "the first layer's 256-unit tiles differ"
-    # one K-tile per LDS stage (the round-4 loop) against two (the default)
-    ks1 = _run(0, s_config, tmp_path / "ks1.npy", CATEARS_X6_KS="1")
-    assert np.array_equal(ks1, base), "one K-tile per LDS stage differs from two"
+    # two K-tiles per LDS stage against one (the default)
+    ks2 = _run(0, s_config, tmp_path / "ks2.npy", CATEARS_X6_KS="2")
+    assert np.array_equal(ks2, base), "two K-tiles per LDS stage differ from one"
 
 
 def test_unknown_variant_fails_loudly(tmp_path, s_config):
