@@ -41,7 +41,7 @@ constexpr int kFramesPerBlock = 4;  // granularity of the plan's block_utt table
 #define FBANK_WAVES 8
 #endif
 constexpr int kWaves = FBANK_WAVES;  // waves per block (8 frames each)
-constexpr int kBlocksPerCU = kWaves == 8 ? 2 : 3;  // LDS: kWaves x 8 x kStride x 4 B (1072 B) frames + the tables
+constexpr int kBlocksPerCU = kWaves == 8 ? 2 : 3;  // LDS: kWaves x 8 frames x kStride x 4 B (1056 B at 264) + the tables
 
 __device__ __forceinline__ void wave_sync() { wave_lds_sync(); }
 
