@@ -68,12 +68,20 @@ __global__ __launch_bounds__(kWaves * 64, 4) void fbank_kernel(const FbankTables
                                                             const int64_t *__restrict__ frame_off,
                                                             const int *__restrict__ block_utt, int64_t total_frames,
                                                             float *__restrict__ feats, float *__restrict__ mel_out) {
-  __shared__ __attribute__((aligned(16))) float lds[kWaves * kLanes * kStride];
-  __shared__ __attribute__((aligned(16))) Fb8Lds T;
+  // the tables first: their addresses (a per-lane base plus constants) stay
+  // below 64 KB, inside the ds_read immediate offset; behind the 66 KB of
+  // frames each table access needed its own address VALU
+  struct Smem {
+    Fb8Lds T;
+    float frames[kWaves * kLanes * kStride];
+  };
+  __shared__ __attribute__((aligned(16))) Smem sm;
   // kBlocksPerCU blocks must fit the CU's 160 KB of LDS, or occupancy drops
   // silently (the launch bound would still allow them)
-  static_assert(kBlocksPerCU * (sizeof(float) * kWaves * kLanes * kStride + sizeof(Fb8Lds)) <= 160 * 1024,
-                "fbank_kernel: LDS for kBlocksPerCU blocks exceeds 160 KB");
+  static_assert(kBlocksPerCU * sizeof(Smem) <= 160 * 1024, "fbank_kernel: LDS for kBlocksPerCU blocks exceeds 160 KB");
+  static_assert(sizeof(Fb8Lds) % 16 == 0 && sizeof(Fb8Lds) < 64 * 1024, "tables: 16-byte frames, immediate offsets");
+  Fb8Lds &T = sm.T;
+  float *lds = sm.frames;
   for (int i = threadIdx.x; i < kOpsA * kLanes * kTwA; i += kWaves * 64) T.twa[i] = tab->fb8_twa[i];
   for (int i = threadIdx.x; i < kWinLen; i += kWaves * 64) T.win[i] = tab->window[i];
   for (int i = threadIdx.x; i < 2 * 129; i += kWaves * 64) T.kn[i] = tab->kn[i];
@@ -94,8 +102,12 @@ __global__ __launch_bounds__(kWaves * 64, 4) void fbank_kernel(const FbankTables
     asm volatile("" : "+v"(lane));
     const int r = lane & 7, fs = lane >> 3;
     float *fbuf = lds + (wave * kLanes + fs) * kStride;
-    const int64_t f = g * kLanes + fs;
-    const int64_t fc = f < total_frames ? f : total_frames - 1;
+    // lanes past the last frame take the last frame: the clamp as a
+    // wave-uniform bound on fs (a 64-bit select against a uniform value kept
+    // that value in a VGPR, which went to scratch)
+    const int64_t left = total_frames - 1 - g * kLanes;  // >= 0 inside the loop
+    const int last_fs = (int)(left < kLanes - 1 ? left : kLanes - 1);
+    const int64_t fc = g * kLanes + (fs < last_fs ? fs : last_fs);
     int u = block_utt[fc / kFramesPerBlock];
     while (fc >= frame_off[u + 1]) ++u;
     const Sample *src = pcm + sample_off[u] + (fc - frame_off[u]) * kShift;
