@@ -58,6 +58,9 @@ $(OBJ)/gemm_bf16x6.o: HIPFLAGS += -fno-slp-vectorize $(X6FLAGS)
 # pushed it into scratch
 $(OBJ)/fbank.o: HIPFLAGS += -fno-slp-vectorize
 
+# CMVNFLAGS: experiment defines for the CMVN kernel (e.g. -DCMVN_TILE=48)
+$(OBJ)/cmvn.o: HIPFLAGS += $(CMVNFLAGS)
+
 # the fast fbank mode is not bit-exact by design: let it contract mul/add
 $(OBJ)/fbank_fast.o: HIPFLAGS += -ffp-contract=fast $(FFDIAG)
 
