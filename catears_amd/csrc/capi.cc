@@ -1022,9 +1022,30 @@ int ce_gpu_plan_destroy(ce_gpu_plan *p) {
   return CE_GPU_OK;
 }
 
+}  // extern "C"
+
+// CATEARS_SKIP (measurement builds only, -DCATEARS_DIAG: wrong results, timing
+// only): launches left out of every call, to price each stage of a pipeline
+// by its absence -- 1 first GEMM layer, 2 finalize, 4 fbank, 8 CMVN, 16 last
+// GEMM layer, 32 the hidden GEMM layers.  0 in the product library.
+static int diag_skip() {
+#ifdef CATEARS_DIAG
+  static const int v = [] {
+    const char *e = getenv("CATEARS_SKIP");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+#else
+  return 0;
+#endif
+}
+
+extern "C" {
+
 int ce_gpu_fbank(ce_gpu_ctx *ctx, const ce_gpu_plan *p, const float *d_pcm, float *d_feats, float *d_mel) {
   if (!ctx || !p || (p->total_frames > 0 && (!d_pcm || !d_feats))) return fail(CE_GPU_EINVAL, "NULL argument");
   ProfScope prof(ctx, CE_GPU_PROF_FBANK);
+  if (diag_skip() & 4) return CE_GPU_OK;
   const FbankTables *t = ctx->d_tables.as<FbankTables>();
   return ctx->fbank_mode == CE_GPU_FBANK_FAST ? launch_fbank_fast(ctx->stream, t, p, d_pcm, d_feats, d_mel)
                                               : launch_fbank(ctx->stream, t, p, d_pcm, d_feats, d_mel);
@@ -1046,6 +1067,7 @@ int ce_gpu_cmvn(ce_gpu_ctx *ctx, const ce_gpu_plan *p, const float *d_global_sta
   const size_t bytes = (size_t)p->total_frames * kMel * sizeof(float);
   if (bytes && a < b + bytes && b < a + bytes) return fail(CE_GPU_EINVAL, "cmvn: d_out overlaps d_feats");
   ProfScope prof(ctx, CE_GPU_PROF_CMVN);
+  if (diag_skip() & 8) return CE_GPU_OK;
   return launch_cmvn(ctx->stream, p, d_global_stats, d_feats, d_out);
 }
 
@@ -1238,7 +1260,7 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
         CE_TRY(ensure_lat_part(ctx, pf));
         if (last && lat_fused_final()) a.tail = tail;  // the reduce may run inside the finalize
         CE_TRY(launch_gemm_bf16x6_lat(ctx->stream, a, ctx->lat_part.as<float>(), pf));
-      } else {
+      } else if (!(diag_skip() & (i == 0 ? 1 : last ? 16 : 32))) {
         CE_TRY(launch_gemm_bf16x6(ctx->stream, a));
       }
     }
@@ -1499,6 +1521,7 @@ static bool lat_tail_ok(const float *out, const float *log_prior) {
 static int finalize_output(ce_gpu_ctx *ctx, const float *y, int ldy, int first, int rows, int dim,
                            bool log_softmax, const float *log_prior, const int *row_dst, float *out,
                            const LatTail &tail = LatTail()) {
+  if (diag_skip() & 2) return CE_GPU_OK;
   if (tail.active) return launch_lat_finalize(ctx->stream, tail, first, rows, log_softmax, log_prior, row_dst, out);
   return launch_finalize(ctx->stream, y + (size_t)first * ldy, ldy, rows, dim, log_softmax, log_prior, row_dst,
                          out);

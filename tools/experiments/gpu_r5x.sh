@@ -4,21 +4,22 @@
 # pre-warm (x2), C4 with the stage profile, and the exact fbank's PMC
 # counters.  Usage: bash tools/experiments/gpu_r5x.sh
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-cd "$R" && mkdir -p gpurun_out/r05x
-TAG=r05x bash tools/round_gpu.sh > gpurun_out/r05x_round.log 2>&1 || { tail -30 gpurun_out/r05x_round.log; exit 1; }
-tail -32 gpurun_out/r05x_round.log
+T=${T:-r05x}
+cd "$R" && mkdir -p gpurun_out/$T
+TAG=$T bash tools/round_gpu.sh > gpurun_out/${T}_round.log 2>&1 || { tail -30 gpurun_out/${T}_round.log; exit 1; }
+tail -32 gpurun_out/${T}_round.log
 cd "$R" || exit 1
-timeout -k 10 200 python tools/latency.py 200 > gpurun_out/r05x/latency.txt 2>&1 || exit 1
-grep "rows    70" gpurun_out/r05x/latency.txt
+timeout -k 10 200 python tools/latency.py 200 > gpurun_out/$T/latency.txt 2>&1 || exit 1
+grep "rows    70" gpurun_out/$T/latency.txt
 for i in 1 2 3; do
-  timeout -k 10 200 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/r05x/driver_$i.json 2>/dev/null || exit 1
-  cut -c1-170 gpurun_out/r05x/driver_$i.json
+  timeout -k 10 200 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/$T/driver_$i.json 2>/dev/null || exit 1
+  cut -c1-170 gpurun_out/$T/driver_$i.json
 done
 for i in 1 2; do
-  timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --prewarm-ms 0 > gpurun_out/r05x/noprewarm_$i.json 2>/dev/null || exit 1
-  cut -c1-120 gpurun_out/r05x/noprewarm_$i.json
+  timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --prewarm-ms 0 > gpurun_out/$T/noprewarm_$i.json 2>/dev/null || exit 1
+  cut -c1-120 gpurun_out/$T/noprewarm_$i.json
 done
-timeout -k 10 300 python bench.py --workload c4 --no-cpu-baseline --stage-profile > gpurun_out/r05x/c4.json 2> gpurun_out/r05x/c4.err || { tail -5 gpurun_out/r05x/c4.err; exit 1; }
-python3 -c "import json; l=json.load(open('gpurun_out/r05x/c4.json')); print('c4', l['value'], l['roofline']['frac'], json.dumps(l.get('stages')))"
-KREGEX=fbank WORKLOAD=c2 OUT=r05x/pmc_fb bash tools/pmc_kernel.sh > gpurun_out/r05x/pmc_fb.txt 2>&1 || { tail -20 gpurun_out/r05x/pmc_fb.txt; exit 1; }
-tail -30 gpurun_out/r05x/pmc_fb.txt
+timeout -k 10 300 python bench.py --workload c4 --no-cpu-baseline --stage-profile > gpurun_out/$T/c4.json 2> gpurun_out/$T/c4.err || { tail -5 gpurun_out/$T/c4.err; exit 1; }
+python3 -c "import json; l=json.load(open('gpurun_out/$T/c4.json')); print('c4', l['value'], l['roofline']['frac'], json.dumps(l.get('stages')))"
+KREGEX=fbank WORKLOAD=c2 OUT=$T/pmc_fb bash tools/pmc_kernel.sh > gpurun_out/$T/pmc_fb.txt 2>&1 || { tail -20 gpurun_out/$T/pmc_fb.txt; exit 1; }
+tail -30 gpurun_out/$T/pmc_fb.txt
