@@ -98,7 +98,7 @@ int ce_gpu_ctx_overflow(ce_gpu_ctx *ctx, int *overflow);
  * count depends on K and N only, so results do not depend on the row count
  * and propagate_blocks still returns each block exactly the rows it gets
  * alone.  Results differ from the default mode's only by fp32 summation
- * order.  Measured on MI355X (TDNN-S, one stream): 93 us per 70-row chunk
+ * order.  Measured on MI355X (TDNN-S, one stream): 92 us per 70-row chunk
  * (761 us in the default mode), 390 us per 1018-row utterance (780 us);
  * past ~2000 rows the default mode is faster.  Off (0, the default) is the
  * throughput mode for full 4096-row batches. */
@@ -110,7 +110,7 @@ int ce_gpu_ctx_set_latency(ce_gpu_ctx *ctx, int on);
  *       bit-identical to Fbank::Process, log-mel within 1e-5;
  *   CE_GPU_FBANK_FAST  a four-step 16 x 16 FFT with 16 lanes per frame and
  *       tabled twiddles (since round 5 no faster than the exact kernel on
- *       C2: 2.15 vs 2.2 G frames/s; kept as an option): log-mel within
+ *       C2: 2.15 vs 2.27 G frames/s; kept as an option): log-mel within
  *       1e-4 of the reference on speech (and of its Kaldi dump), and as close
  *       to the exact float64 result as the reference's own fp32 order is
  *       (max 7.8e-5 vs the reference's 1.07e-4, p99.9 2.0e-5;
