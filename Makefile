@@ -61,8 +61,10 @@ $(OBJ)/fbank.o: HIPFLAGS += -fno-slp-vectorize
 # CMVNFLAGS: experiment defines for the CMVN kernel (e.g. -DCMVN_TILE=48)
 $(OBJ)/cmvn.o: HIPFLAGS += $(CMVNFLAGS)
 
-# the fast fbank mode is not bit-exact by design: let it contract mul/add
-$(OBJ)/fbank_fast.o: HIPFLAGS += -ffp-contract=fast $(FFDIAG)
+# the fast fbank mode (fbank.hip's lane program again) is not bit-exact by
+# design: let it contract mul/add
+$(OBJ)/fbank_fma.o: HIPFLAGS += -ffp-contract=fast -fno-slp-vectorize
+$(OBJ)/fbank_fma.o: $(SRC)/kernels/fbank.hip
 
 $(OBJ)/%.o: $(SRC)/kernels/%.hip $(HDRS) Makefile
 	@mkdir -p $(OBJ)

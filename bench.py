@@ -108,7 +108,7 @@ def parse(argv=None):
                     help="c3, tests only: use this rank's PCM pool (one process reproducing one rank)")
     ap.add_argument("--fbank", choices=["exact", "fast"], default="exact",
                     help="fbank kernel (ce_gpu_ctx_set_fbank): exact = the reference's operation order "
-                         "(bit-exact pre-log mel), fast = four-step FFT within 3e-5 on log-mel")
+                         "(bit-exact pre-log mel), fast = the same lane program with FMA contraction (not bit-exact; as close to the exact result as the reference)")
     ap.add_argument("--pcm", choices=["f32", "s16"], default="f32",
                     help="resident PCM format: f32 (raw int16 scale floats, WaveReader's output) or s16 "
                          "(the WAV payload; ce_gpu_fbank_s16 converts exactly in the kernel)")
@@ -500,7 +500,7 @@ def main_c2(args):
     if iv:
         avg_ms = sum(b - a for a, b in iv) / len(iv)
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-        kname = ("fbank_fast_kernel" if args.fbank == "fast" else "fbank_kernel") + ("<short*" if s16 else "<float*")
+        kname = ("fbank_fma_kernel" if args.fbank == "fast" else "fbank_kernel") + ("<short*" if s16 else "<float*")
         traffic, src = pmc_traffic(kname, "c2")
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,

@@ -1047,7 +1047,7 @@ int ce_gpu_fbank(ce_gpu_ctx *ctx, const ce_gpu_plan *p, const float *d_pcm, floa
   ProfScope prof(ctx, CE_GPU_PROF_FBANK);
   if (diag_skip() & 4) return CE_GPU_OK;
   const FbankTables *t = ctx->d_tables.as<FbankTables>();
-  return ctx->fbank_mode == CE_GPU_FBANK_FAST ? launch_fbank_fast(ctx->stream, t, p, d_pcm, d_feats, d_mel)
+  return ctx->fbank_mode == CE_GPU_FBANK_FAST ? launch_fbank_fma(ctx->stream, t, p, d_pcm, d_feats, d_mel)
                                               : launch_fbank(ctx->stream, t, p, d_pcm, d_feats, d_mel);
 }
 
@@ -1055,7 +1055,7 @@ int ce_gpu_fbank_s16(ce_gpu_ctx *ctx, const ce_gpu_plan *p, const int16_t *d_pcm
   if (!ctx || !p || (p->total_frames > 0 && (!d_pcm || !d_feats))) return fail(CE_GPU_EINVAL, "NULL argument");
   ProfScope prof(ctx, CE_GPU_PROF_FBANK);
   const FbankTables *t = ctx->d_tables.as<FbankTables>();
-  return ctx->fbank_mode == CE_GPU_FBANK_FAST ? launch_fbank_fast_s16(ctx->stream, t, p, d_pcm, d_feats, d_mel)
+  return ctx->fbank_mode == CE_GPU_FBANK_FAST ? launch_fbank_fma_s16(ctx->stream, t, p, d_pcm, d_feats, d_mel)
                                               : launch_fbank_s16(ctx->stream, t, p, d_pcm, d_feats, d_mel);
 }
 

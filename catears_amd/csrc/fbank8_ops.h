@@ -391,8 +391,17 @@ CE_HD void lane_window(const Sample *src, float mean, int r, const float *win, f
     const int e = 16 * j + 2 * r;
     const float de = (float)src[e] - mean, dod = (float)src[e + 1] - mean;
     const float dp = (float)src[e > 0 ? e - 1 : 0] - mean;
+#ifdef FB8_FMA
+    // fast mode: 0.97f and one fused rounding instead of the double product;
+    // the loads in groups of five pairs (all 75 samples' loads hoisted ahead
+    // took the kernel past 128 registers)
+    re[j] = __builtin_fmaf(-0.97f, dp, de) * win[e];
+    im[j] = __builtin_fmaf(-0.97f, de, dod) * win[e + 1];
+    if (j % 5 == 4) CE_SCHED_FENCE();
+#else
     re[j] = fb::preemph(de, dp) * win[e];
     im[j] = fb::preemph(dod, de) * win[e + 1];
+#endif
   }
   CE_UNROLL
   for (int j = kSamp; j < kPts; ++j) re[j] = im[j] = 0.0f;

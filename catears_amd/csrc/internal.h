@@ -78,17 +78,6 @@ struct FbankTables {
   int mel_wbase[kMel];              // start of its weights in mel_w
   float mel_w[512];                 // 492 nonzero weights in total
   int mel_total;
-  // fast mode (kernels/fbank_fast.hip: four-step 16 x 16 FFT, 16 lanes per
-  // frame; not the reference's operation order, <= 3e-5 on log-mel)
-  float ff_tw[16 * 16 * 2];         // W256^(n2 k1) = (cos, -sin)(2 pi n2 k1 / 256) at [k1][n2]
-  float ff_post[kHalf * 2];         // W512^k = (cos, -sin)(2 pi k / 512), k = 0..255
-  // mel in three slots (kFfSlot): lane j of a frame forms band ff_slot_band[q
-  // * 16 + j] of slot q (-1: none) over a fixed window of kFfSlot[q] bins
-  // starting at ff_slot_start[...] (kept inside 0..255), weights zero outside
-  // the band -- fixed trip counts, so the kernel's dots are straight-line code
-  int ff_slot_band[3 * 16];
-  int ff_slot_start[3 * 16];
-  float ff_slot_w[16 * 52];  // lane j's windows back to back at j * kFfSlotW
   // exact kernel (fbank8_ops.h): phase-A twiddle records [op][lane r][8],
   // the length-16 node's twiddles (n = 1, n = 3), mel slot windows: lane q
   // of slot c starts at bin fb8_mel_st[c * 8 + q], weights at
@@ -98,12 +87,6 @@ struct FbankTables {
   int fb8_mel_st[5 * 8];
   float fb8_mel_w[92 * 8];
 };
-
-// fast-mode mel slot windows (bins): the 16 longest bands (<= 31 bins), the
-// next 16 (<= 12), the last 8 (<= 5); multiples of 4 for 16-byte weight reads
-constexpr int kFfSlot[3] = {32, 12, 8};
-constexpr int kFfSlotBase[3] = {0, 32, 44};
-constexpr int kFfSlotW = 52;
 
 // Builds the tables (tables.cc).
 void build_fbank_tables(FbankTables *t);
@@ -424,10 +407,11 @@ int launch_fbank(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, 
 int launch_fbank_s16(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, const int16_t *pcm,
                      float *feats, float *mel);
 // fast mode (ce_gpu_ctx_set_fbank(ctx, CE_GPU_FBANK_FAST))
-int launch_fbank_fast(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, const float *pcm,
-                      float *feats, float *mel);
-int launch_fbank_fast_s16(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, const int16_t *pcm,
-                          float *feats, float *mel);
+// the fast mode: fbank.hip's lane program with FMA contraction (fbank_fma.hip)
+int launch_fbank_fma(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, const float *pcm, float *feats,
+                     float *mel);
+int launch_fbank_fma_s16(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, const int16_t *pcm,
+                         float *feats, float *mel);
 int launch_cmvn(hipStream_t s, const ce_gpu_plan *p, const float *gstats, const float *in,
                 float *out);
 

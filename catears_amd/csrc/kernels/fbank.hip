@@ -31,6 +31,18 @@
 #include "../fbank8_ops.h"
 #include "../internal.h"
 
+// FB8_FMA (kernels/fbank_fma.hip): the same lane program built with FMA
+// contraction and a single-precision pre-emphasis -- the fast mode
+#ifdef FB8_FMA
+#define FB8_KERNEL fbank_fma_kernel
+#define FB8_LAUNCH launch_fbank_fma
+#define FB8_LAUNCH_S16 launch_fbank_fma_s16
+#else
+#define FB8_KERNEL fbank_kernel
+#define FB8_LAUNCH launch_fbank
+#define FB8_LAUNCH_S16 launch_fbank_s16
+#endif
+
 namespace catears {
 namespace {
 
@@ -62,7 +74,7 @@ struct Fb8Lds {
 // MEL: also store the pre-log mel energies (a template argument: a branch on
 // the pointer inside the frame loop cost ~57 registers)
 template <typename Sample, bool MEL>
-__global__ __launch_bounds__(kWaves * 64, 4) void fbank_kernel(const FbankTables *__restrict__ tab,
+__global__ __launch_bounds__(kWaves * 64, 4) void FB8_KERNEL(const FbankTables *__restrict__ tab,
                                                             const Sample *__restrict__ pcm,
                                                             const int64_t *__restrict__ sample_off,
                                                             const int64_t *__restrict__ frame_off,
@@ -179,11 +191,11 @@ int launch_fbank_t(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p
   const int64_t max_blocks = 256 * kBlocksPerCU;
   const unsigned grid = (unsigned)(blocks < max_blocks ? blocks : max_blocks);
   if (mel)
-    hipLaunchKernelGGL((fbank_kernel<Sample, true>), dim3(grid), dim3(kWaves * 64), 0, s, d_tab, pcm,
+    hipLaunchKernelGGL((FB8_KERNEL<Sample, true>), dim3(grid), dim3(kWaves * 64), 0, s, d_tab, pcm,
                      p->d_sample_off.as<int64_t>(), p->d_frame_off.as<int64_t>(),
                      p->d_block_utt.as<int>(), p->total_frames, feats, mel);
     else
-    hipLaunchKernelGGL((fbank_kernel<Sample, false>), dim3(grid), dim3(kWaves * 64), 0, s, d_tab, pcm,
+    hipLaunchKernelGGL((FB8_KERNEL<Sample, false>), dim3(grid), dim3(kWaves * 64), 0, s, d_tab, pcm,
                      p->d_sample_off.as<int64_t>(), p->d_frame_off.as<int64_t>(),
                      p->d_block_utt.as<int>(), p->total_frames, feats, mel);
   CE_HIP(hipGetLastError());
@@ -192,16 +204,18 @@ int launch_fbank_t(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p
 
 }  // namespace
 
-int launch_fbank(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, const float *pcm,
-                 float *feats, float *mel) {
+int FB8_LAUNCH(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, const float *pcm, float *feats,
+               float *mel) {
   return launch_fbank_t(s, d_tab, p, pcm, feats, mel);
 }
 
-int launch_fbank_s16(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, const int16_t *pcm,
-                     float *feats, float *mel) {
+int FB8_LAUNCH_S16(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, const int16_t *pcm,
+                   float *feats, float *mel) {
   return launch_fbank_t(s, d_tab, p, pcm, feats, mel);
 }
 
+#ifndef FB8_FMA
 int fbank_frames_per_block() { return kFramesPerBlock; }
+#endif
 
 }  // namespace catears

@@ -105,41 +105,6 @@ void build_post_twiddles(FbankTables *t) {
   }
 }
 
-// Fast-mode tables: the four-step FFT's inter-pass twiddles, the real-FFT
-// post twiddles (both in double, rounded once) and the 40 mel bands in three
-// fixed-size slots of a frame's 16 lanes (zero-padded weight windows).
-void build_fast(FbankTables *t) {
-  const double tau = 6.283185307179586476925286766559005;
-  for (int k1 = 0; k1 < 16; ++k1)
-    for (int n2 = 0; n2 < 16; ++n2) {
-      const double a = tau * n2 * k1 / 256.0;
-      t->ff_tw[2 * (k1 * 16 + n2)] = (float)cos(a);
-      t->ff_tw[2 * (k1 * 16 + n2) + 1] = (float)-sin(a);
-    }
-  for (int k = 0; k < kHalf; ++k) {
-    const double a = tau * k / 512.0;
-    t->ff_post[2 * k] = (float)cos(a);
-    t->ff_post[2 * k + 1] = (float)-sin(a);
-  }
-  // bands by length, longest first: ranks 0-15 fill slot 0, 16-31 slot 1,
-  // 32-39 slot 2 (lane = rank mod 16)
-  std::vector<int> order(kMel);
-  for (int b = 0; b < kMel; ++b) order[b] = b;
-  std::sort(order.begin(), order.end(), [&](int a, int b) {
-    return t->mel_len[a] != t->mel_len[b] ? t->mel_len[a] > t->mel_len[b] : a < b;
-  });
-  for (int i = 0; i < 3 * 16; ++i) t->ff_slot_band[i] = -1, t->ff_slot_start[i] = 0;
-  for (int r = 0; r < kMel; ++r) {
-    const int q = r / 16, j = r % 16, b = order[r], bound = kFfSlot[q];
-    if (t->mel_len[b] > bound || t->mel_off[b] < 0) abort();  // the geometry is fixed (src/fbank.h)
-    const int start = std::min(t->mel_off[b], kHalf - bound);
-    t->ff_slot_band[q * 16 + j] = b;
-    t->ff_slot_start[q * 16 + j] = start;
-    float *w = t->ff_slot_w + j * kFfSlotW + kFfSlotBase[q] + (t->mel_off[b] - start);
-    for (int i = 0; i < t->mel_len[b]; ++i) w[i] = t->mel_w[t->mel_wbase[b] + i];
-  }
-}
-
 // Exact-kernel tables (fbank8_ops.h): each lane's phase-A twiddle records,
 // the length-16 node's, and the mel slot windows.
 void build_fb8(FbankTables *t) {
@@ -176,7 +141,6 @@ void build_fbank_tables(FbankTables *t) {
   build_mel(t);
   build_twiddles(t);
   build_post_twiddles(t);
-  build_fast(t);
   build_fb8(t);
 }
 

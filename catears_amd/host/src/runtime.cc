@@ -115,9 +115,9 @@ Runtime::Runtime() {
     if (v < 1 || v > 16) throw DeviceError("CATEARS_LANES must be 1..16");
     max_lanes_ = v;
   }
-  // CATEARS_FBANK=fast: every lane's fbank launches take the four-step-FFT
-  // kernel (ce_gpu_ctx_set_fbank); "exact" (the default) keeps the
-  // reference's operation order
+  // CATEARS_FBANK=fast: every lane's fbank launches take the fast kernel
+  // (the exact lane program with FMA contraction, ce_gpu_ctx_set_fbank);
+  // "exact" (the default) keeps the reference's operation order
   if (const char *e = getenv("CATEARS_FBANK")) {
     const std::string v(e);
     if (v == "fast")

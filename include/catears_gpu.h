@@ -108,17 +108,18 @@ int ce_gpu_ctx_set_latency(ce_gpu_ctx *ctx, int on);
  *   CE_GPU_FBANK_EXACT (default) the reference's operation order
  *       (src/fbank.cc:44-245, src/srfft.cc:124-459): pre-log mel energies
  *       bit-identical to Fbank::Process, log-mel within 1e-5;
- *   CE_GPU_FBANK_FAST  a four-step 16 x 16 FFT with 16 lanes per frame and
- *       tabled twiddles (since round 5 no faster than the exact kernel on
- *       C2: 2.15 vs 2.27 G frames/s; kept as an option): log-mel within
+ *   CE_GPU_FBANK_FAST  the exact kernel's lane program built with FMA
+ *       contraction and a single-precision pre-emphasis (23 % fewer
+ *       instructions; C2 2.53 vs 2.26 G frames/s on one MI355X): log-mel within
  *       1e-4 of the reference on speech (and of its Kaldi dump), and as close
  *       to the exact float64 result as the reference's own fp32 order is
- *       (max 7.8e-5 vs the reference's 1.07e-4, p99.9 2.0e-5;
+ *       (max 1.03e-4 vs the reference's 1.07e-4, p99.9 2.7e-5;
  *       tests/test_gpu_fbank_fast.py).  Deterministic: a frame's features
  *       do not depend on the batch it is computed in, nor on the kernels
  *       that run beside it on other streams (bit-identical to a serial
  *       re-score in the pipelined bench, tests/test_gpu_determinism.py;
- *       round 4's build missed this in ~2 % of launches). */
+ *       round 4's four-step fast kernel missed this in ~2 % of launches,
+ *       DESIGN.md §8b). */
 #define CE_GPU_FBANK_EXACT 0
 #define CE_GPU_FBANK_FAST 1
 int ce_gpu_ctx_set_fbank(ce_gpu_ctx *ctx, int mode);

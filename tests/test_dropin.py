@@ -142,7 +142,7 @@ def test_fbank_streaming_matches_oracle(tmp_path, oracle, chunk):
 
 @pytest.mark.gpu
 def test_fbank_fast_mode_through_the_dropin(tmp_path, oracle):
-    """CATEARS_FBANK=fast selects the four-step-FFT kernel for every lane of
+    """CATEARS_FBANK=fast selects the fast (FMA-contracted) kernel for every lane of
     the drop-in runtime: streaming Fbank::Process output within the north
     star's fbank tolerance of the oracle and the Kaldi dump; an unknown value
     is refused (DeviceError, nonzero exit)."""

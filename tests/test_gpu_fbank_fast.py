@@ -1,7 +1,9 @@
 """The fast fbank mode (ce_gpu_ctx_set_fbank(ctx, CE_GPU_FBANK_FAST),
-kernels/fbank_fast.hip): a four-step 16 x 16 FFT with 16 lanes per frame
-instead of the reference's split-radix order, so its bar is the north star's
-fbank tolerance rather than bit-exactness.
+kernels/fbank_fma.hip): the exact kernel's lane program built with FMA
+contraction and a single-precision pre-emphasis, so its products and sums
+round differently from the reference's and its bar is the north star's
+fbank tolerance rather than bit-exactness.  (Rounds 3-4 ran a four-step
+16 x 16 FFT here; the contracted lane program is faster and as accurate.)
 
 Two yardsticks.  (1) The oracle (the reference's fp32 arithmetic): log-mel
 within 1e-4 on the reference's speech WAVs (the reference
