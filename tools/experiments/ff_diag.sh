@@ -1,3 +1,6 @@
+# (Historical: measures the four-step fast fbank kernel, kernels/fbank_fast.hip, removed
+# in round 5 when the fast mode became the contracted exact lane program; kept as the
+# record of DESIGN.md §8b.  It no longer builds against the current tree.)
 # Fast-fbank run-to-run difference: the stress (lds_race_stress.py) over the
 # FF_DIAG builds of fbank_fast.hip (make lib OBJ=build/obj_ffdN
 # LIB=catears_amd/lib/ab/libffdN.so FFDIAG=-DFF_DIAG=N).

@@ -1,3 +1,6 @@
+# (Historical: measures the four-step fast fbank kernel, kernels/fbank_fast.hip, removed
+# in round 5 when the fast mode became the contracted exact lane program; kept as the
+# record of DESIGN.md §8b.  It no longer builds against the current tree.)
 # fast fbank instruction mix and stalls (two PMC passes over C2 fast, 3 steps)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(pwd)}" && mkdir -p gpurun_out/ffpmc && export TMPDIR=/tmp
