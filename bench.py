@@ -626,6 +626,10 @@ def main_c4(args):
     gat = RowGather(counts, pdfs, torch.float32, "cuda", depth=nbuf, keep=dump is not None) if gather else None
     comm = torch.cuda.Stream() if gather else None
     checksum = torch.zeros((), dtype=torch.float64, device="cuda")
+    # one process: each nnet stream folds its own batches into its own
+    # accumulator (ce_gpu_sum_f64; no two streams touch one)
+    sums = [torch.zeros((), dtype=torch.float64, device="cuda") for _ in range(NB)]
+    parts = [torch.empty(gpu.SUM_PARTS, dtype=torch.float64, device="cuda") for _ in range(NB)]
 
     def front_stage(i):
         slot = i % F
@@ -662,7 +666,7 @@ def main_c4(args):
         else:
             # one process: consume every row the same way rank 0 does
             with torch.cuda.stream(stream):
-                checksum.add_(torch.sum(outs[o][:n], dtype=torch.float64))
+                gpu.sum_f64(outs[o][:n], sums[b], parts[b])
         if dump is not None and (rank == 0) and any(int(u) % args.c4_dump_every == 0 for u in batches[i]):
             stream.synchronize()
             _c4_keep(dump, batches[i], frames, outs[o][:n].cpu().numpy(), args.c4_dump_every)
@@ -711,6 +715,8 @@ def main_c4(args):
         elapsed = float(t.item())
     if gat is not None:
         checksum += gat.checksum
+    for v in sums:
+        checksum += v
     rows_in = gat.rows_in if gat is not None else 0
     busy = None
     n_gemm = 0
@@ -941,6 +947,7 @@ def main(argv=None):
     comm = torch.cuda.Stream() if gather else None
     checksum = torch.zeros((), dtype=torch.float64, device="cuda")
     fold = [torch.zeros((), dtype=torch.float64, device="cuda") for _ in backs] if args.fold_all else None
+    fold_parts = [torch.empty(gpu.SUM_PARTS, dtype=torch.float64, device="cuda") for _ in backs] if args.fold_all else None
     dump = {} if args.c3_dump else None  # step -> device copy of this rank's rows
     kept = {} if args.verify_serial else None  # step -> (fbank out, CMVN out, per-row sums) as pipelined
     # --host-io: a host caller's buffers.  PCM slots on the device are
@@ -995,7 +1002,7 @@ def main(argv=None):
             # this slot as soon as it is)
             with torch.cuda.stream(stream):
                 if fold is not None:
-                    fold[b] += outs[o].double().sum()
+                    gpu.sum_f64(outs[o], fold[b], fold_parts[b])
                 if dump is not None:
                     dump[i] = outs[o].clone()
                     if os.environ.get("CATEARS_DUMP_FEATS"):

@@ -1867,6 +1867,13 @@ int ce_gpu_loglik_columns(ce_gpu_ctx *ctx, const float *d_loglik, int rows, int 
   return launch_loglik_columns(ctx->stream, d_loglik, rows, ld, dim, d_cols, n_cols, d_out);
 }
 
+int ce_gpu_sum_f64(void *stream, const float *d_x, int64_t n, double *d_part, double *d_acc) {
+  if (n < 0) return fail(CE_GPU_EINVAL, "bad argument");
+  if (n == 0) return CE_GPU_OK;
+  if (!d_x || !d_part || !d_acc) return fail(CE_GPU_EINVAL, "NULL argument");
+  return launch_sum_f64(reinterpret_cast<hipStream_t>(stream), d_x, n, d_part, d_acc);
+}
+
 int ce_gpu_model_quantize(ce_gpu_ctx *ctx, ce_gpu_model *m) {
   if (!ctx || !m) return fail(CE_GPU_EINVAL, "NULL argument");
   if (m->int8) return CE_GPU_OK;

@@ -11,6 +11,7 @@
 //   reference's converter, but legal NN02).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "../internal.h"
@@ -309,6 +310,74 @@ int launch_loglik_columns(hipStream_t s, const float *ll, int rows, int ld, int 
                           int n_cols, float *out) {
   if (rows > 0 && n_cols > 0)
     hipLaunchKernelGGL(loglik_columns_kernel, dim3(rows), dim3(256), 0, s, ll, ld, dim, cols, n_cols, out);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
+}
+
+namespace {
+
+// Float64 sum of n floats (ce_gpu_sum_f64): each thread adds its strided
+// float4s in double -- four accumulators, one per load slot, so four loads
+// are in flight per thread -- then a fixed wave / block tree, one partial per
+// block, and one wave folds the partials in block order.  The order depends
+// on n only: the same bytes give the same double.
+constexpr int kSumThreads = 256;
+
+template <bool V4>
+__global__ __launch_bounds__(kSumThreads) void sum_f64_kernel(const float *__restrict__ x, int64_t n,
+                                                              double *__restrict__ part) {
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * kSumThreads, t = (int64_t)blockIdx.x * kSumThreads + threadIdx.x;
+  if (V4) {
+    const float4 *x4 = reinterpret_cast<const float4 *>(x);
+    const int64_t n4 = n >> 2;
+    int64_t i = t;
+    for (; i + 3 * stride < n4; i += 4 * stride) {
+      const float4 a = x4[i], b = x4[i + stride], c = x4[i + 2 * stride], d = x4[i + 3 * stride];
+      s0 += (((double)a.x + (double)a.y) + (double)a.z) + (double)a.w;
+      s1 += (((double)b.x + (double)b.y) + (double)b.z) + (double)b.w;
+      s2 += (((double)c.x + (double)c.y) + (double)c.z) + (double)c.w;
+      s3 += (((double)d.x + (double)d.y) + (double)d.z) + (double)d.w;
+    }
+    for (; i < n4; i += stride) {
+      const float4 a = x4[i];
+      s0 += (((double)a.x + (double)a.y) + (double)a.z) + (double)a.w;
+    }
+    if (t < (n & 3)) s1 += (double)x[(n4 << 2) + t];
+  } else {
+    for (int64_t i = t; i < n; i += stride) s0 += (double)x[i];
+  }
+  double s = (s0 + s1) + (s2 + s3);
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
+  __shared__ double ws[kSumThreads / 64];
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = ((ws[0] + ws[1]) + ws[2]) + ws[3];
+}
+
+__global__ __launch_bounds__(64) void sum_parts_kernel(const double *__restrict__ part, int nparts,
+                                                       double *__restrict__ acc) {
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += 64) s += part[i];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
+  if (threadIdx.x == 0) *acc += s;
+}
+
+}  // namespace
+
+int launch_sum_f64(hipStream_t s, const float *x, int64_t n, double *part, double *acc) {
+  if (n <= 0) return CE_GPU_OK;
+  const bool v4 = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  const int64_t units = v4 ? (n >> 2) : n, want = (units + 4 * kSumThreads - 1) / (4 * kSumThreads);
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(want, CE_GPU_SUM_PARTS));
+  if (v4)
+    hipLaunchKernelGGL(sum_f64_kernel<true>, dim3(blocks), dim3(kSumThreads), 0, s, x, n, part);
+  else
+    hipLaunchKernelGGL(sum_f64_kernel<false>, dim3(blocks), dim3(kSumThreads), 0, s, x, n, part);
+  CE_HIP(hipGetLastError());
+  hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(64), 0, s, part, blocks, acc);
   CE_HIP(hipGetLastError());
   return CE_GPU_OK;
 }

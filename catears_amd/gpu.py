@@ -31,7 +31,7 @@ ABI = [
     "ce_gpu_profile_anchor", "ce_gpu_ctx_profile_intervals", "ce_gpu_model_quantize",
     "ce_gpu_nnet_propagate_blocks", "ce_gpu_loglik_gather", "ce_gpu_loglik_columns",
     "ce_gpu_model_set_gemm", "ce_gpu_model_get_gemm", "ce_gpu_ctx_overflow", "ce_gpu_ctx_set_latency",
-    "ce_gpu_fbank_s16", "ce_gpu_score_s16", "ce_gpu_ctx_set_fbank",
+    "ce_gpu_fbank_s16", "ce_gpu_score_s16", "ce_gpu_ctx_set_fbank", "ce_gpu_sum_f64",
 ]
 
 # ce_gpu_model_set_gemm modes
@@ -103,6 +103,7 @@ def lib():
         "ce_gpu_ctx_overflow": (ci, [vp, pi]),
         "ce_gpu_ctx_set_latency": (ci, [vp, ci]),
         "ce_gpu_ctx_set_fbank": (ci, [vp, ci]),
+        "ce_gpu_sum_f64": (ci, [vp, vp, i64, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -416,6 +417,22 @@ def loglik_columns(ctx, loglik, cols, out=None):
     check(lib().ce_gpu_loglik_columns(ctx.h, _ptr(loglik), loglik.shape[0], loglik.stride(0), loglik.shape[1],
                                       _ptr(cols), int(cols.numel()), _ptr(out)))
     return out
+
+
+SUM_PARTS = 1024  # CE_GPU_SUM_PARTS
+
+
+def sum_f64(x, acc, part):
+    """ce_gpu_sum_f64 on torch's current stream: acc (a 0-d float64 device
+    tensor) += the float64 sum of the contiguous float32 tensor x; part: a
+    float64 device tensor of >= SUM_PARTS elements (scratch, stream-ordered)."""
+    import torch
+    assert x.dtype == torch.float32 and x.is_contiguous() and x.is_cuda
+    assert acc.dtype == torch.float64 and acc.numel() == 1 and part.dtype == torch.float64
+    assert part.numel() >= SUM_PARTS
+    stream = torch.cuda.current_stream(x.device).cuda_stream
+    check(lib().ce_gpu_sum_f64(stream, _ptr(x), x.numel(), _ptr(part), _ptr(acc)))
+    return acc
 
 
 def sgemm(ctx, a, b, c=None):

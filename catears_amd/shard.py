@@ -113,6 +113,11 @@ class RowGather:
             self.recv = [[torch.empty((max(rows[p], 1), width), dtype=dtype, device=rdev) for p in range(self.world)]
                          for _ in range(depth)]
         self.sums = [torch.zeros((), dtype=torch.float64, device=self.device) for _ in range(depth)]
+        # device folds run ce_gpu_sum_f64 (HBM speed; torch's float64 sum runs
+        # at about a third of it): scratch per slot, as a slot's folds are
+        # ordered on one stream
+        self.parts = ([torch.empty(1024, dtype=torch.float64, device=self.device) for _ in range(depth)]
+                      if self.device.type == "cuda" else None)
         self.rows_in = 0       # rows rank 0 received
         self.batches = 0       # steps retired
         self.keep = [] if keep else None  # (peer, step, host rows) -- tests only
@@ -166,21 +171,29 @@ class RowGather:
                     b = self.recv[slot][p][:n]
                     bufs.append((p, b))
                     ops.append(dist.P2POp(dist.irecv, b, p, self.group))
-            acc = self.sums[slot]
+            acc, part = self.sums[slot], self.parts[slot] if self.parts is not None else None
 
             def after():
                 for p, b in bufs:
                     x = b.to(self.device, non_blocking=False) if self.staged else b
-                    acc.add_(torch.sum(x, dtype=torch.float64))
+                    self._fold(x, acc, part)
                     self.rows_in += b.shape[0]
                     if self.keep is not None:
                         self.keep.append((p, s, b.cpu().numpy().copy()))
             if own is not None:
-                acc.add_(torch.sum(own, dtype=torch.float64))
+                self._fold(own, acc, part)
         works = dist.batch_isend_irecv(ops) if ops else []
         stream = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
         self.pending[slot] = (works, after, stream)
         return slot
+
+    @staticmethod
+    def _fold(x, acc, part):
+        if x.is_cuda:
+            from catears_amd import gpu
+            gpu.sum_f64(x.contiguous(), acc, part)
+        else:
+            acc.add_(torch.sum(x, dtype=torch.float64))
 
     def wait_slot(self, slot):
         """Order the current stream (NCCL) or the host (gloo) after the

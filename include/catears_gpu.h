@@ -402,6 +402,17 @@ int ce_gpu_loglik_gather(ce_gpu_ctx *ctx, const float *d_loglik, int rows, int l
 int ce_gpu_loglik_columns(ce_gpu_ctx *ctx, const float *d_loglik, int rows, int ld, int dim,
                           const int32_t *d_cols, int n_cols, float *d_out);
 
+/* *d_acc += the float64 sum of the n floats at d_x, on `stream` (a
+ * hipStream_t; NULL = the null stream) of the current device; d_part is
+ * device scratch for CE_GPU_SUM_PARTS doubles.  Each element is widened to
+ * double before it is added, in an order that depends on n only (the same
+ * bytes give the same sum).  No reference counterpart: the consumer of the
+ * log-likelihood rows gathered to rank 0 -- bench.py and
+ * catears_amd/shard.py RowGather fold every row into this checksum, at HBM
+ * speed where torch's float64 reduction runs at about a third of it. */
+#define CE_GPU_SUM_PARTS 1024
+int ce_gpu_sum_f64(void *stream, const float *d_x, int64_t n, double *d_part, double *d_acc);
+
 #ifdef __cplusplus
 }  /* extern "C" */
 #endif
