@@ -23,3 +23,9 @@ timeout -k 10 300 python bench.py --workload c4 --no-cpu-baseline --stage-profil
 python3 -c "import json; l=json.load(open('gpurun_out/$T/c4.json')); print('c4', l['value'], l['roofline']['frac'], json.dumps(l.get('stages')))"
 KREGEX=fbank WORKLOAD=c2 OUT=$T/pmc_fb bash tools/pmc_kernel.sh > gpurun_out/$T/pmc_fb.txt 2>&1 || { tail -20 gpurun_out/$T/pmc_fb.txt; exit 1; }
 tail -30 gpurun_out/$T/pmc_fb.txt
+timeout -k 10 200 python bench.py --no-cpu-baseline > gpurun_out/$T/default.json 2>/dev/null || exit 1
+cut -c1-120 gpurun_out/$T/default.json
+timeout -k 10 200 python bench.py --workload c2 --fbank fast --steps 30 --warmup 3 --no-cpu-baseline > gpurun_out/$T/c2_fast.json 2>/dev/null || exit 1
+cut -c1-120 gpurun_out/$T/c2_fast.json
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/$T/smoke.log 2>&1 || { tail -5 gpurun_out/$T/smoke.log; exit 1; }
+tail -1 gpurun_out/$T/smoke.log
