@@ -269,6 +269,27 @@ def pmc_traffic(kernel, workload="c3"):
     return round(sum(v["hbm_bytes_per_launch"] * v["dispatches"] for v in hits) / n), os.path.relpath(files[-1], ROOT)
 
 
+CLOCK_GHZ = 2.4  # MI355X peak engine clock (MI355X_MICROARCH.md)
+
+
+def pmc_valu(kernel):
+    """SQ_INSTS_VALU of `kernel` per C2 launch from the newest committed
+    exact-fbank PMC summary (tools/pmc_kernel.sh over `--workload c2`, the
+    998 000-frame launch); None if there is none or the kernel is not in it."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_c2_pmc_fbank*.txt")), reverse=True)
+    base = kernel.split("<")[0]
+    tmpl = kernel.split("<")[1].rstrip("*") if "<" in kernel else ""
+    for f in files:  # the newest summary that has this kernel
+        name = None
+        for ln in open(f):
+            if ln.startswith("void "):
+                name = ln.strip()[5:]
+            elif "SQ_INSTS_VALU" in ln and name and kernel_match(name, base + "*") and tmpl.split("*")[0] in name:
+                return {"instructions": float(ln.split()[-1]), "frames": 998000, "source": os.path.relpath(f, ROOT)}
+    return None
+
+
 def pmc_mfma(kernel, workload="c3"):
     """Matrix-pipe utilisation of `kernel` from the newest committed
     rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE summary
@@ -507,6 +528,17 @@ def main_c2(args):
                     "kernel": kname, "launches": len(iv), "avg_launch_ms": round(avg_ms, 4),
                     "algorithmic_bytes_per_launch": bytes_per_launch,
                     "valu_flops_per_frame": 14000}
+        # the bound the kernel actually meets: VALU issue (PMC instruction
+        # count of the committed kernel x 4 cycles per wave64 instruction on
+        # a 16-lane SIMD, over the 1024 SIMDs, against this launch's time)
+        valu = pmc_valu(kname)
+        if valu is not None:
+            n_launch = valu["frames"]
+            instr = valu["instructions"] * plan.total_frames / n_launch
+            need_ms = instr * 4 / 1024 / (CLOCK_GHZ * 1e6)
+            roofline["valu_issue"] = {"instructions_per_launch": round(instr), "ms_at_issue_rate": round(need_ms, 4),
+                                      "frac": round(need_ms / avg_ms, 3), "clock_ghz": CLOCK_GHZ,
+                                      "source": valu["source"]}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         threads, how = usable_cores()

@@ -29,3 +29,5 @@ timeout -k 10 200 python bench.py --workload c2 --fbank fast --steps 30 --warmup
 cut -c1-120 gpurun_out/$T/c2_fast.json
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/$T/smoke.log 2>&1 || { tail -5 gpurun_out/$T/smoke.log; exit 1; }
 tail -1 gpurun_out/$T/smoke.log
+KREGEX=fbank_fma WORKLOAD=c2 OUT=$T/pmc_fbf BENCH_ARGS="--fbank fast" bash tools/pmc_kernel.sh > gpurun_out/$T/pmc_fbf.txt 2>&1 || { tail -20 gpurun_out/$T/pmc_fbf.txt; exit 1; }
+tail -14 gpurun_out/$T/pmc_fbf.txt

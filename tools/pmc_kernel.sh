@@ -1,5 +1,5 @@
 # PMC counter groups for one kernel of one bench workload (no tracing).
-# KREGEX=fbank WORKLOAD=c2 OUT=pmcf bash tools/pmc_kernel.sh
+# KREGEX=fbank WORKLOAD=c2 OUT=pmcf [BENCH_ARGS="--fbank fast"] bash tools/pmc_kernel.sh
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=${OUT:-pmck}
 mkdir -p "$R/gpurun_out/$OUT"
@@ -12,7 +12,7 @@ for grp in "${PG[@]}" ${EXTRA_GROUPS}; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp --kernel-include-regex "${KREGEX:-fbank}" --output-format csv \
       -d "$R/gpurun_out/$OUT/p$i" -o run -- \
-      python "$R/bench.py" --workload ${WORKLOAD:-c2} --steps 3 --warmup 1 --no-cpu-baseline --no-profile \
+      python "$R/bench.py" --workload ${WORKLOAD:-c2} --steps 3 --warmup 1 --no-cpu-baseline --no-profile ${BENCH_ARGS} \
       > "$R/gpurun_out/$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -20 "$R/gpurun_out/$OUT/p$i.log"; exit 1; }
 done
 python3 - "$R/gpurun_out/$OUT" <<'PY'
