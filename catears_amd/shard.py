@@ -116,8 +116,10 @@ class RowGather:
         # device folds run ce_gpu_sum_f64 (HBM speed; torch's float64 sum runs
         # at about a third of it): scratch per slot, as a slot's folds are
         # ordered on one stream
-        self.parts = ([torch.empty(1024, dtype=torch.float64, device=self.device) for _ in range(depth)]
-                      if self.device.type == "cuda" else None)
+        self.parts = None
+        if self.device.type == "cuda":
+            from catears_amd import gpu
+            self.parts = [torch.empty(gpu.SUM_PARTS, dtype=torch.float64, device=self.device) for _ in range(depth)]
         self.rows_in = 0       # rows rank 0 received
         self.batches = 0       # steps retired
         self.keep = [] if keep else None  # (peer, step, host rows) -- tests only

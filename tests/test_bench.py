@@ -57,6 +57,17 @@ def test_roofline_kernels_have_committed_mfma_util(bench, workload, kernel):
     assert 0.0 < u["chip"] <= u["active_cus"] <= 1.0
 
 
+@pytest.mark.parametrize("kernel", ["fbank_kernel<float*", "fbank_fma_kernel<float*"])
+def test_c2_valu_issue_counts_are_committed(bench, kernel):
+    """C2's VALU-issue roofline (roofline.valu_issue) reads the committed PMC
+    instruction count of both fbank kernels; a renamed kernel or a missing
+    summary would silently drop it."""
+    v = bench.pmc_valu(kernel)
+    assert v is not None, f"no committed c2 PMC summary with {kernel}"
+    # a few hundred wave instructions per frame for the exact lane program
+    assert 100 < v["instructions"] / v["frames"] < 400
+
+
 def _clean_env(**extra):
     import os
     env = {k: v for k, v in os.environ.items()
