@@ -117,6 +117,11 @@ def parse(argv=None):
                          "the library's (bf16x6: three exact bf16 planes, six products, fp32 GEMM)")
     ap.add_argument("--front-streams", type=int, default=1,
                     help="fbank + CMVN streams; consecutive batches alternate between them")
+    ap.add_argument("--rehearse-peers", type=int, default=0,
+                    help="c3, one process, measurement only: after each batch, copy it into K receive buffers "
+                         "and fold all K+1 (ce_gpu_sum_f64) on a stream of its own -- rank 0's per-step receive "
+                         "and fold load at N = K+1 ranks, on one GPU (the copies read and write locally, more "
+                         "than the peers' remote writes cost rank 0)")
     ap.add_argument("--launch-check", action="store_true",
                     help="tests only: start and check the N ranks (self-launch, world size, gloo process group) "
                          "and print a line with n_gpus and the ranks seen, without touching a GPU")
@@ -978,6 +983,13 @@ def main(argv=None):
                         keep=bool(args.c3_dump) and rank == 0)
     comm = torch.cuda.Stream() if gather else None
     checksum = torch.zeros((), dtype=torch.float64, device="cuda")
+    reh = None
+    if args.rehearse_peers:
+        assert world == 1 and not gather, "--rehearse-peers rehearses rank 0 in one process"
+        reh = {"stream": torch.cuda.Stream(), "done": [None] * nbuf,
+               "recv": [torch.empty_like(outs[0]) for _ in range(args.rehearse_peers)],
+               "acc": torch.zeros((), dtype=torch.float64, device="cuda"),
+               "part": torch.empty(gpu.SUM_PARTS, dtype=torch.float64, device="cuda")}
     fold = [torch.zeros((), dtype=torch.float64, device="cuda") for _ in backs] if args.fold_all else None
     fold_parts = [torch.empty(gpu.SUM_PARTS, dtype=torch.float64, device="cuda") for _ in backs] if args.fold_all else None
     dump = {} if args.c3_dump else None  # step -> device copy of this rank's rows
@@ -1025,6 +1037,8 @@ def main(argv=None):
                 gat.wait_slot(o)
         if done[o] is not None:
             stream.wait_event(done[o])  # the batch nbuf steps ago (maybe another stream) wrote outs[o]
+        if reh is not None and reh["done"][o] is not None:
+            stream.wait_event(reh["done"][o])  # the rehearsed receives have read outs[o]
         if hio is not None and hio["down_done"][o] is not None:
             stream.wait_event(hio["down_done"][o])  # ... and its log-likelihoods are on the host
         stream.wait_event(ready[slot])
@@ -1056,6 +1070,18 @@ def main(argv=None):
             dv = torch.cuda.Event()
             dv.record(down)
             hio["down_done"][o] = dv
+        if reh is not None:
+            rs = reh["stream"]
+            rs.wait_event(ev)
+            with torch.cuda.stream(rs):
+                if not os.environ.get("CATEARS_REHEARSE_NOCOPY"):
+                    for r in reh["recv"]:
+                        r.copy_(outs[o])
+                # the step's rows as RowGather folds them: own + every peer's, one launch pair
+                gpu.sum_f64_many([outs[o]] + reh["recv"], reh["acc"], reh["part"])
+                rev = torch.cuda.Event()
+                rev.record(rs)
+                reh["done"][o] = rev
         if gat is not None:
             # the transfer is enqueued from a stream of its own that waits
             # for this batch only, so the nnet streams never wait on each
@@ -1295,6 +1321,10 @@ def main(argv=None):
         line["verify"] = verify
         if verify_ranks is not None:
             line["verify_ranks"] = verify_ranks
+    if args.rehearse_peers:
+        line["rehearse_peers"] = {"peers": args.rehearse_peers,
+                                  "what": "rank 0's receive copies and float64 folds of N = peers + 1 ranks, "
+                                          "on a stream of its own; measurement only"}
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

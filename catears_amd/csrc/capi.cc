@@ -1868,10 +1868,22 @@ int ce_gpu_loglik_columns(ce_gpu_ctx *ctx, const float *d_loglik, int rows, int 
 }
 
 int ce_gpu_sum_f64(void *stream, const float *d_x, int64_t n, double *d_part, double *d_acc) {
-  if (n < 0) return fail(CE_GPU_EINVAL, "bad argument");
-  if (n == 0) return CE_GPU_OK;
-  if (!d_x || !d_part || !d_acc) return fail(CE_GPU_EINVAL, "NULL argument");
-  return launch_sum_f64(reinterpret_cast<hipStream_t>(stream), d_x, n, d_part, d_acc);
+  return ce_gpu_sum_f64_many(stream, 1, &d_x, &n, d_part, d_acc);
+}
+
+int ce_gpu_sum_f64_many(void *stream, int count, const float *const *d_x, const int64_t *n, double *d_part,
+                        double *d_acc) {
+  if (count < 0 || count > CE_GPU_SUM_MAX_BUFS || (count > 0 && (!d_x || !n)))
+    return fail(CE_GPU_EINVAL, "sum_f64: bad buffer list");
+  bool any = false;
+  for (int k = 0; k < count; ++k) {
+    if (n[k] < 0) return fail(CE_GPU_EINVAL, "bad argument");
+    if (n[k] > 0 && !d_x[k]) return fail(CE_GPU_EINVAL, "NULL argument");
+    any = any || n[k] > 0;
+  }
+  if (!any) return CE_GPU_OK;
+  if (!d_part || !d_acc) return fail(CE_GPU_EINVAL, "NULL argument");
+  return launch_sum_f64(reinterpret_cast<hipStream_t>(stream), count, d_x, n, d_part, d_acc);
 }
 
 int ce_gpu_model_quantize(ce_gpu_ctx *ctx, ce_gpu_model *m) {

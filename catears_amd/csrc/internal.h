@@ -503,7 +503,7 @@ int launch_loglik_gather(hipStream_t s, const float *ll, int rows, int ld, int d
                          const int32_t *row, const int32_t *trans, int n, float scale, float *out);
 int launch_loglik_columns(hipStream_t s, const float *ll, int rows, int ld, int dim, const int32_t *cols,
                           int n_cols, float *out);
-int launch_sum_f64(hipStream_t s, const float *x, int64_t n, double *part, double *acc);
+int launch_sum_f64(hipStream_t s, int count, const float *const *x, const int64_t *n, double *part, double *acc);
 int launch_rowop_raw(hipStream_t s, int kind, int dim, const float *scale, const float *offset, float *x,
                      int ldx, int rows);
 int launch_splice(hipStream_t s, int rows, int dim, const float *in, int ld_in, const int32_t *h_idx,

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "../internal.h"
@@ -316,36 +317,48 @@ int launch_loglik_columns(hipStream_t s, const float *ll, int rows, int ld, int 
 
 namespace {
 
-// Float64 sum of n floats (ce_gpu_sum_f64): each thread adds its strided
-// float4s in double -- four accumulators, one per load slot, so four loads
-// are in flight per thread -- then a fixed wave / block tree, one partial per
+// Float64 sum of up to kSumMaxBufs float buffers (ce_gpu_sum_f64 /
+// ce_gpu_sum_f64_many): each thread adds its strided float4s of every
+// buffer in double -- four accumulators, one per load slot, so four loads are
+// in flight per thread -- then a fixed wave / block tree, one partial per
 // block, and one wave folds the partials in block order.  The order depends
-// on n only: the same bytes give the same double.
+// on the buffer sizes only: the same bytes give the same double.  Several
+// buffers share one launch pair (rank 0 folds every peer's rows of a step
+// at once).
 constexpr int kSumThreads = 256;
+constexpr int kSumMaxBufs = 16;
 
-template <bool V4>
-__global__ __launch_bounds__(kSumThreads) void sum_f64_kernel(const float *__restrict__ x, int64_t n,
-                                                              double *__restrict__ part) {
+struct SumBufs {
+  const float *x[kSumMaxBufs];
+  int64_t n[kSumMaxBufs];
+  int count;
+};
+
+__global__ __launch_bounds__(kSumThreads) void sum_f64_kernel(SumBufs bufs, double *__restrict__ part) {
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
   const int64_t stride = (int64_t)gridDim.x * kSumThreads, t = (int64_t)blockIdx.x * kSumThreads + threadIdx.x;
-  if (V4) {
-    const float4 *x4 = reinterpret_cast<const float4 *>(x);
-    const int64_t n4 = n >> 2;
-    int64_t i = t;
-    for (; i + 3 * stride < n4; i += 4 * stride) {
-      const float4 a = x4[i], b = x4[i + stride], c = x4[i + 2 * stride], d = x4[i + 3 * stride];
-      s0 += (((double)a.x + (double)a.y) + (double)a.z) + (double)a.w;
-      s1 += (((double)b.x + (double)b.y) + (double)b.z) + (double)b.w;
-      s2 += (((double)c.x + (double)c.y) + (double)c.z) + (double)c.w;
-      s3 += (((double)d.x + (double)d.y) + (double)d.z) + (double)d.w;
+  for (int k = 0; k < bufs.count; ++k) {
+    const float *x = bufs.x[k];
+    const int64_t n = bufs.n[k];
+    if ((reinterpret_cast<uintptr_t>(x) & 15) == 0) {  // uniform per buffer
+      const float4 *x4 = reinterpret_cast<const float4 *>(x);
+      const int64_t n4 = n >> 2;
+      int64_t i = t;
+      for (; i + 3 * stride < n4; i += 4 * stride) {
+        const float4 a = x4[i], b = x4[i + stride], c = x4[i + 2 * stride], d = x4[i + 3 * stride];
+        s0 += (((double)a.x + (double)a.y) + (double)a.z) + (double)a.w;
+        s1 += (((double)b.x + (double)b.y) + (double)b.z) + (double)b.w;
+        s2 += (((double)c.x + (double)c.y) + (double)c.z) + (double)c.w;
+        s3 += (((double)d.x + (double)d.y) + (double)d.z) + (double)d.w;
+      }
+      for (; i < n4; i += stride) {
+        const float4 a = x4[i];
+        s0 += (((double)a.x + (double)a.y) + (double)a.z) + (double)a.w;
+      }
+      if (t < (n & 3)) s1 += (double)x[(n4 << 2) + t];
+    } else {
+      for (int64_t i = t; i < n; i += stride) s0 += (double)x[i];
     }
-    for (; i < n4; i += stride) {
-      const float4 a = x4[i];
-      s0 += (((double)a.x + (double)a.y) + (double)a.z) + (double)a.w;
-    }
-    if (t < (n & 3)) s1 += (double)x[(n4 << 2) + t];
-  } else {
-    for (int64_t i = t; i < n; i += stride) s0 += (double)x[i];
   }
   double s = (s0 + s1) + (s2 + s3);
 #pragma unroll
@@ -367,15 +380,26 @@ __global__ __launch_bounds__(64) void sum_parts_kernel(const double *__restrict_
 
 }  // namespace
 
-int launch_sum_f64(hipStream_t s, const float *x, int64_t n, double *part, double *acc) {
-  if (n <= 0) return CE_GPU_OK;
-  const bool v4 = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
-  const int64_t units = v4 ? (n >> 2) : n, want = (units + 4 * kSumThreads - 1) / (4 * kSumThreads);
-  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(want, CE_GPU_SUM_PARTS));
-  if (v4)
-    hipLaunchKernelGGL(sum_f64_kernel<true>, dim3(blocks), dim3(kSumThreads), 0, s, x, n, part);
-  else
-    hipLaunchKernelGGL(sum_f64_kernel<false>, dim3(blocks), dim3(kSumThreads), 0, s, x, n, part);
+int launch_sum_f64(hipStream_t s, int count, const float *const *x, const int64_t *n, double *part, double *acc) {
+  if (count < 0 || count > kSumMaxBufs) return fail(CE_GPU_EINVAL, "sum_f64: 0..16 buffers per call");
+  SumBufs b{};
+  int64_t units = 0;
+  for (int k = 0; k < count; ++k) {
+    if (n[k] <= 0) continue;
+    b.x[b.count] = x[k];
+    b.n[b.count] = n[k];
+    ++b.count;
+    units = std::max<int64_t>(units, n[k] >> 2);
+  }
+  if (b.count == 0) return CE_GPU_OK;
+  static const int cap = [] {  // CATEARS_SUM_BLOCKS: fewer blocks, for measurement
+    const char *e = getenv("CATEARS_SUM_BLOCKS");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 && v <= CE_GPU_SUM_PARTS ? v : CE_GPU_SUM_PARTS;
+  }();
+  const int64_t want = (std::max<int64_t>(units, 1) + 4 * kSumThreads - 1) / (4 * kSumThreads);
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(want, cap));
+  hipLaunchKernelGGL(sum_f64_kernel, dim3(blocks), dim3(kSumThreads), 0, s, b, part);
   CE_HIP(hipGetLastError());
   hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(64), 0, s, part, blocks, acc);
   CE_HIP(hipGetLastError());

@@ -32,6 +32,7 @@ ABI = [
     "ce_gpu_nnet_propagate_blocks", "ce_gpu_loglik_gather", "ce_gpu_loglik_columns",
     "ce_gpu_model_set_gemm", "ce_gpu_model_get_gemm", "ce_gpu_ctx_overflow", "ce_gpu_ctx_set_latency",
     "ce_gpu_fbank_s16", "ce_gpu_score_s16", "ce_gpu_ctx_set_fbank", "ce_gpu_sum_f64",
+    "ce_gpu_sum_f64_many",
 ]
 
 # ce_gpu_model_set_gemm modes
@@ -104,6 +105,7 @@ def lib():
         "ce_gpu_ctx_set_latency": (ci, [vp, ci]),
         "ce_gpu_ctx_set_fbank": (ci, [vp, ci]),
         "ce_gpu_sum_f64": (ci, [vp, vp, i64, vp, vp]),
+        "ce_gpu_sum_f64_many": (ci, [vp, ci, ctypes.POINTER(vp), pi64, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -432,6 +434,27 @@ def sum_f64(x, acc, part):
     assert part.numel() >= SUM_PARTS
     stream = torch.cuda.current_stream(x.device).cuda_stream
     check(lib().ce_gpu_sum_f64(stream, _ptr(x), x.numel(), _ptr(part), _ptr(acc)))
+    return acc
+
+
+SUM_MAX_BUFS = 16  # CE_GPU_SUM_MAX_BUFS
+
+
+def sum_f64_many(xs, acc, part):
+    """ce_gpu_sum_f64_many on torch's current stream: acc += the float64 sum
+    of every contiguous float32 tensor in xs, SUM_MAX_BUFS at a time (one
+    launch pair per group)."""
+    import torch
+    assert acc.dtype == torch.float64 and acc.numel() == 1 and part.dtype == torch.float64
+    assert part.numel() >= SUM_PARTS
+    stream = torch.cuda.current_stream(acc.device).cuda_stream
+    for g in range(0, len(xs), SUM_MAX_BUFS):
+        grp = xs[g:g + SUM_MAX_BUFS]
+        for x in grp:
+            assert x.dtype == torch.float32 and x.is_contiguous() and x.is_cuda
+        ptrs = (ctypes.c_void_p * len(grp))(*[_ptr(x) for x in grp])
+        ns = (ctypes.c_int64 * len(grp))(*[x.numel() for x in grp])
+        check(lib().ce_gpu_sum_f64_many(stream, len(grp), ptrs, ns, _ptr(part), _ptr(acc)))
     return acc
 
 

@@ -176,26 +176,29 @@ class RowGather:
             acc, part = self.sums[slot], self.parts[slot] if self.parts is not None else None
 
             def after():
+                # every peer's rows of this step (and rank 0's own) in one fold
+                xs = [own] if own is not None else []
                 for p, b in bufs:
-                    x = b.to(self.device, non_blocking=False) if self.staged else b
-                    self._fold(x, acc, part)
+                    xs.append(b.to(self.device, non_blocking=False) if self.staged else b)
                     self.rows_in += b.shape[0]
                     if self.keep is not None:
                         self.keep.append((p, s, b.cpu().numpy().copy()))
-            if own is not None:
-                self._fold(own, acc, part)
+                self._fold(xs, acc, part)
         works = dist.batch_isend_irecv(ops) if ops else []
         stream = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
         self.pending[slot] = (works, after, stream)
         return slot
 
     @staticmethod
-    def _fold(x, acc, part):
-        if x.is_cuda:
+    def _fold(xs, acc, part):
+        if not xs:
+            return
+        if xs[0].is_cuda:
             from catears_amd import gpu
-            gpu.sum_f64(x.contiguous(), acc, part)
+            gpu.sum_f64_many([x.contiguous() for x in xs], acc, part)
         else:
-            acc.add_(torch.sum(x, dtype=torch.float64))
+            for x in xs:
+                acc.add_(torch.sum(x, dtype=torch.float64))
 
     def wait_slot(self, slot):
         """Order the current stream (NCCL) or the host (gloo) after the

@@ -412,6 +412,12 @@ int ce_gpu_loglik_columns(ce_gpu_ctx *ctx, const float *d_loglik, int rows, int 
  * speed where torch's float64 reduction runs at about a third of it. */
 #define CE_GPU_SUM_PARTS 1024
 int ce_gpu_sum_f64(void *stream, const float *d_x, int64_t n, double *d_part, double *d_acc);
+/* The same over up to CE_GPU_SUM_MAX_BUFS buffers in one launch pair (host
+ * arrays of device pointers and lengths): rank 0 folds every peer's rows of a
+ * step at once, without a launch per peer. */
+#define CE_GPU_SUM_MAX_BUFS 16
+int ce_gpu_sum_f64_many(void *stream, int count, const float *const *d_x, const int64_t *n, double *d_part,
+                        double *d_acc);
 
 #ifdef __cplusplus
 }  /* extern "C" */
