@@ -117,6 +117,10 @@ def parse(argv=None):
                          "the library's (bf16x6: three exact bf16 planes, six products, fp32 GEMM)")
     ap.add_argument("--front-streams", type=int, default=1,
                     help="fbank + CMVN streams; consecutive batches alternate between them")
+    ap.add_argument("--sink-share", type=float, default=None,
+                    help="c3, N > 1: the fraction of steps rank 0 scores a batch of its own (it also receives "
+                         "and folds every peer's rows).  Default: 1 - 0.054 (N - 1), at least 0.5, on RCCL "
+                         "(the per-peer receive + fold cost measured by --rehearse-peers, DESIGN.md §7); 1 on gloo")
     ap.add_argument("--rehearse-peers", type=int, default=0,
                     help="c3, one process, measurement only: after each batch, copy it into K receive buffers "
                          "and fold all K+1 (ce_gpu_sum_f64) on a stream of its own -- rank 0's per-step receive "
@@ -1092,12 +1096,33 @@ def main(argv=None):
                     dump[i] = outs[o].clone()
                 assert gat.submit(i, outs[o], own=outs[o] if rank == 0 else None) == o
 
+    # rank 0 hosts the gather sink: at N > 1 it scores a batch on a share of
+    # the steps only (evenly spread) and on the others just receives and
+    # folds its peers' rows
+    share = 1.0
+    if gather and rank == 0:
+        share = args.sink_share if args.sink_share is not None else (
+            max(0.5, 1.0 - 0.054 * (world - 1)) if args.dist_backend == "nccl" else 1.0)
+        assert 0.0 < share <= 1.0, "--sink-share must be in (0, 1]"
+
+    def scores(i):
+        return share >= 1.0 or int((i + 1) * share) > int(i * share)
+
     def run(first, count):
-        front_stage(first)
+        todo = [i for i in range(first, first + count) if scores(i)]
+        if todo:
+            front_stage(todo[0])
+        k = 0
         for i in range(first, first + count):
-            if i + 1 < first + count:
-                front_stage(i + 1)
+            if not scores(i):
+                if gat is not None:  # rank 0: this step's receives only
+                    with torch.cuda.stream(comm):
+                        gat.submit(i, None)
+                continue
+            if k + 1 < len(todo):
+                front_stage(todo[k + 1])
             back_stage(i)
+            k += 1
 
     # pre-warm: the same steps, nothing gathered, dumped or folded, until the
     # chip has run the loaded pipeline for --prewarm-ms (profiles/r04h_step_times*:
@@ -1176,7 +1201,12 @@ def main(argv=None):
             # (sum of launch durations, launches, wall time the class was on the device)
             prof[name] = (sum(b - a for a, b in iv), len(iv), gpu.union_ms(iv))
 
-    total_frames = frames_per_step * args.steps * world
+    my_steps = sum(1 for i in range(args.warmup, args.warmup + args.steps) if scores(i))
+    total_frames = frames_per_step * my_steps
+    if world > 1:
+        t = torch.tensor([total_frames], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        total_frames = int(t.item())
     value = total_frames / elapsed
     if rank != 0:
         if world > 1:
@@ -1307,7 +1337,9 @@ def main(argv=None):
                    "frames_per_step_per_gpu": frames_per_step, "packed_rows": plan.max_chunk_rows,
                    "cmvn": not args.no_cmvn, "fbank": args.fbank, "pcm": args.pcm, "parallelism": f"utterance shard x{world}",
                    "streams": 1 if args.serial else 1 + NB,
-                   "gather": gather, "host_io": bool(args.host_io)},
+                   "gather": gather, "host_io": bool(args.host_io),
+                   "sink_share": share if gather else None, "rank0_scored_steps": my_steps if gather else None,
+                   "frames_total": total_frames},
         "roofline": roofline, "cpu_baseline": cpu, "stages": stages,
         "end_to_end_mfma_frac": round(value / world * FLOPS_PER_FRAME / 1e12 /
                                       (MFMA_I8_PEAK_TOPS if int8 else

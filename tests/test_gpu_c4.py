@@ -225,3 +225,26 @@ def test_c3_gpus_2_self_launched():
     line = line[0]
     assert line["n_gpus"] == 2 and line["config"]["gather"] and line["finite"]
     assert line["value"] > 0
+
+
+def test_c3_sink_share_rank0_scores_part_of_the_steps(tmp_path):
+    """--sink-share 0.5: rank 0 (the gather sink) scores a batch on every
+    other step and on the rest only receives; the line counts exactly the
+    batches scored, every batch rank 1 sends still arrives bit for bit, and
+    the checksum folds rank 0's own scored batches and every received one."""
+    steps = 6 + 2
+    two = _bench_c3(["--c3-dump", str(tmp_path / "d.npz"), "--sink-share", "0.5"], 2)
+    cfg = two["config"]
+    assert cfg["sink_share"] == 0.5 and cfg["rank0_scored_steps"] == 3  # timed steps 2..7: 3, 5, 7
+    assert cfg["frames_total"] == cfg["frames_per_step_per_gpu"] * (6 + 3)
+    r0, r1 = np.load(tmp_path / "d.rank0.npz"), np.load(tmp_path / "d.rank1.npz")
+    scored = [s for s in range(steps) if int((s + 1) * 0.5) > int(s * 0.5)]
+    assert sorted(f for f in r0.files if f.startswith("r0s")) == sorted(f"r0s{s}" for s in scored)
+    want = 0.0
+    for s in range(steps):
+        sent, got = r1[f"r1s{s}"], r0[f"r1s{s}"]
+        assert np.array_equal(sent.view(np.uint32), got.view(np.uint32)), s
+        want += float(got.astype(np.float64).sum())
+        if s in scored:
+            want += float(r0[f"r0s{s}"].astype(np.float64).sum())
+    assert two["checksum"] == pytest.approx(want, rel=1e-12)
