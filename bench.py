@@ -622,7 +622,13 @@ def main_c4(args):
     # corpus, shard, batches (all deterministic; the row counts are exchanged)
     samples = c4_corpus(args.c4_utts)
     frames = [num_frames(int(n)) for n in samples]
-    mine = shard_utterances(frames, world, rank)
+    # rank 0 receives and folds every peer's rows: on RCCL it takes a smaller
+    # share of the corpus (the same rule as C3's --sink-share)
+    share = 1.0
+    if world > 1 and not args.no_gather:
+        share = args.sink_share if args.sink_share is not None else (
+            max(0.5, 1.0 - 0.054 * (world - 1)) if args.dist_backend == "nccl" else 1.0)
+    mine = shard_utterances(frames, world, rank, weights=[share] + [1.0] * (world - 1))
     batches = [[mine[i] for i in b] for b in pack_batches([frames[u] for u in mine], L, R, 4096)]
     my_rows = [sum(frames[u] for u in b) for b in batches]
     if world > 1:
@@ -823,7 +829,7 @@ def main_c4(args):
                    "frames_per_rank": [int(sum(c)) for c in counts], "batches_per_rank": [len(c) for c in counts],
                    "rows_gathered_to_rank0": int(rows_in), "pcm": args.pcm, "cmvn": not args.no_cmvn,
                    "parallelism": f"utterance shard x{world}", "streams": 1 if args.serial else 1 + NB,
-                   "gather": gather},
+                   "gather": gather, "sink_share": share if gather else None},
         "roofline": roofline, "cpu_baseline": None,
         "checksum": float(checksum.item()),
     }

@@ -47,15 +47,18 @@ def c4_corpus(n_utts=C4_UTTS, seed=20250117):
     return out
 
 
-def shard_utterances(lengths, world, rank):
+def shard_utterances(lengths, world, rank, weights=None):
     """Longest-first greedy assignment by frame count: returns the indices of
     the utterances rank `rank` scores, ascending (deterministic, balanced
-    within one utterance's length)."""
+    within one utterance's length).  weights: each rank's relative capacity
+    (default equal; bench.py gives rank 0, the gather sink, less)."""
+    w = [1.0] * world if weights is None else [float(x) for x in weights]
+    assert len(w) == world and all(x > 0 for x in w)
     order = sorted(range(len(lengths)), key=lambda i: (-int(lengths[i]), i))
     load = [0] * world
     owner = [0] * len(lengths)
     for i in order:
-        r = min(range(world), key=lambda k: (load[k], k))
+        r = min(range(world), key=lambda k: ((load[k] + int(lengths[i])) / w[k], k))
         owner[i] = r
         load[r] += int(lengths[i])
     return [i for i in range(len(lengths)) if owner[i] == rank]

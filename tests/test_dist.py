@@ -25,6 +25,20 @@ def test_shard_covers_and_balances():
     assert shard_utterances(lengths, 2, 0) == shard_utterances(lengths, 2, 0)
 
 
+def test_shard_weights_give_rank0_its_share():
+    """bench.py's sink share: rank 0 weighted 0.62 at 8 ranks gets 0.62 of a
+    peer's frames (within one utterance), every utterance exactly once."""
+    from catears_amd.shard import c4_corpus
+    frames = [num_frames(int(n)) for n in c4_corpus(4000)]
+    w = [0.62] + [1.0] * 7
+    parts = [shard_utterances(frames, 8, r, weights=w) for r in range(8)]
+    assert sorted(i for p in parts for i in p) == list(range(len(frames)))
+    loads = [sum(frames[i] for i in p) for p in parts]
+    peer = sum(loads[1:]) / 7
+    assert abs(loads[0] / peer - 0.62) < 0.01
+    assert max(loads[1:]) - min(loads[1:]) <= max(frames)
+
+
 def test_c4_corpus_is_100h_length_mixed():
     s = c4_corpus()
     assert len(s) == C4_UTTS == 36000
