@@ -12,7 +12,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <cstdlib>
 #include <type_traits>
 
 #include "../internal.h"
@@ -392,13 +391,9 @@ int launch_sum_f64(hipStream_t s, int count, const float *const *x, const int64_
     units = std::max<int64_t>(units, n[k] >> 2);
   }
   if (b.count == 0) return CE_GPU_OK;
-  static const int cap = [] {  // CATEARS_SUM_BLOCKS: fewer blocks, for measurement
-    const char *e = getenv("CATEARS_SUM_BLOCKS");
-    const int v = e ? atoi(e) : 0;
-    return v > 0 && v <= CE_GPU_SUM_PARTS ? v : CE_GPU_SUM_PARTS;
-  }();
+  // (128 or 32 blocks measured no better beside the GEMMs, profiles/r05t_rank0_rehearsal.txt)
   const int64_t want = (std::max<int64_t>(units, 1) + 4 * kSumThreads - 1) / (4 * kSumThreads);
-  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(want, cap));
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(want, CE_GPU_SUM_PARTS));
   hipLaunchKernelGGL(sum_f64_kernel, dim3(blocks), dim3(kSumThreads), 0, s, b, part);
   CE_HIP(hipGetLastError());
   hipLaunchKernelGGL(sum_parts_kernel, dim3(1), dim3(64), 0, s, part, blocks, acc);
