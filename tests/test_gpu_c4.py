@@ -248,3 +248,12 @@ def test_c3_sink_share_rank0_scores_part_of_the_steps(tmp_path):
         if s in scored:
             want += float(r0[f"r0s{s}"].astype(np.float64).sum())
     assert two["checksum"] == pytest.approx(want, rel=1e-12)
+
+
+def test_rehearse_peers_runs_and_reports():
+    """bench.py --rehearse-peers (the one-GPU rehearsal of rank 0's receive +
+    fold load behind the default sink share): it runs the
+    pipeline with the extra copies and folds and says so in the line."""
+    line = _bench_c3(["--rehearse-peers", "2"], 1)
+    assert line["rehearse_peers"]["peers"] == 2 and line["finite"]
+    assert line["config"]["frames_total"] == line["config"]["frames_per_step_per_gpu"] * 6
