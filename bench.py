@@ -998,6 +998,7 @@ def main(argv=None):
         assert world == 1 and not gather, "--rehearse-peers rehearses rank 0 in one process"
         reh = {"stream": torch.cuda.Stream(), "done": [None] * nbuf,
                "recv": [torch.empty_like(outs[0]) for _ in range(args.rehearse_peers)],
+               "src": torch.zeros_like(outs[0]),
                "acc": torch.zeros((), dtype=torch.float64, device="cuda"),
                "part": torch.empty(gpu.SUM_PARTS, dtype=torch.float64, device="cuda")}
     fold = [torch.zeros((), dtype=torch.float64, device="cuda") for _ in backs] if args.fold_all else None
@@ -1110,6 +1111,19 @@ def main(argv=None):
         share = args.sink_share if args.sink_share is not None else (
             max(0.5, 1.0 - 0.054 * (world - 1)) if args.dist_backend == "nccl" else 1.0)
         assert 0.0 < share <= 1.0, "--sink-share must be in (0, 1]"
+    elif reh is not None and args.sink_share is not None:
+        share = args.sink_share  # the rehearsal of rank 0 at that share
+        assert 0.0 < share <= 1.0, "--sink-share must be in (0, 1]"
+
+    def rehearse_receive():
+        # --rehearse-peers, a step that scores no batch of its own: the peers'
+        # receives and their fold only (from a buffer the pipeline never writes)
+        rs = reh["stream"]
+        with torch.cuda.stream(rs):
+            if not os.environ.get("CATEARS_REHEARSE_NOCOPY"):
+                for r in reh["recv"]:
+                    r.copy_(reh["src"])
+            gpu.sum_f64_many(reh["recv"], reh["acc"], reh["part"])
 
     def scores(i):
         return share >= 1.0 or int((i + 1) * share) > int(i * share)
@@ -1124,6 +1138,8 @@ def main(argv=None):
                 if gat is not None:  # rank 0: this step's receives only
                     with torch.cuda.stream(comm):
                         gat.submit(i, None)
+                if reh is not None:
+                    rehearse_receive()
                 continue
             if k + 1 < len(todo):
                 front_stage(todo[k + 1])
