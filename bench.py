@@ -118,14 +118,19 @@ def parse(argv=None):
     ap.add_argument("--front-streams", type=int, default=1,
                     help="fbank + CMVN streams; consecutive batches alternate between them")
     ap.add_argument("--sink-share", type=float, default=None,
-                    help="c3, N > 1: the fraction of steps rank 0 scores a batch of its own (it also receives "
-                         "and folds every peer's rows).  Default: 1 - 0.054 (N - 1), at least 0.5, on RCCL "
-                         "(the per-peer receive + fold cost measured by --rehearse-peers, DESIGN.md §7); 1 on gloo")
+                    help="c3 / c4, N > 1: the fraction of steps (c4: of the corpus share) rank 0 scores a batch "
+                         "of its own (it also receives and folds every peer's rows).  Default on RCCL: "
+                         "min(1, 1.066 - 0.055 (N - 1)), at least 0.5 (rank 0's receive + fold load and a sender's "
+                         "send read, measured by --rehearse-peers / --rehearse-send, DESIGN.md §7); 1 on gloo")
     ap.add_argument("--rehearse-peers", type=int, default=0,
                     help="c3, one process, measurement only: after each batch, copy it into K receive buffers "
                          "and fold all K+1 (ce_gpu_sum_f64) on a stream of its own -- rank 0's per-step receive "
                          "and fold load at N = K+1 ranks, on one GPU (the copies read and write locally, more "
                          "than the peers' remote writes cost rank 0)")
+    ap.add_argument("--rehearse-send", action="store_true",
+                    help="c3, one process, measurement only: read every batch once more after it is scored "
+                         "(float64 fold on a stream of its own) -- a sender's local cost of handing its rows "
+                         "to RCCL at N > 1")
     ap.add_argument("--launch-check", action="store_true",
                     help="tests only: start and check the N ranks (self-launch, world size, gloo process group) "
                          "and print a line with n_gpus and the ranks seen, without touching a GPU")
@@ -276,6 +281,15 @@ def pmc_traffic(kernel, workload="c3"):
         return None, None
     n = sum(v["dispatches"] for v in hits)
     return round(sum(v["hbm_bytes_per_launch"] * v["dispatches"] for v in hits) / n), os.path.relpath(files[-1], ROOT)
+
+
+def sink_share_default(world):
+    """Rank 0's share of the scoring at `world` ranks on RCCL:
+    from the one-GPU rehearsals, rank 0's step grows about 0.034 ms per peer
+    whose rows it receives and folds (--rehearse-peers), a sender's about
+    0.04 ms for handing its batch over (--rehearse-send), on a 0.61 ms step;
+    equal step times give 1 + (0.04 - 0.034 (N - 1)) / 0.61."""
+    return max(0.5, min(1.0, 1.066 - 0.055 * (world - 1)))
 
 
 CLOCK_GHZ = 2.4  # MI355X peak engine clock (MI355X_MICROARCH.md)
@@ -627,7 +641,7 @@ def main_c4(args):
     share = 1.0
     if world > 1 and not args.no_gather:
         share = args.sink_share if args.sink_share is not None else (
-            max(0.5, 1.0 - 0.054 * (world - 1)) if args.dist_backend == "nccl" else 1.0)
+            sink_share_default(world) if args.dist_backend == "nccl" else 1.0)
     mine = shard_utterances(frames, world, rank, weights=[share] + [1.0] * (world - 1))
     batches = [[mine[i] for i in b] for b in pack_batches([frames[u] for u in mine], L, R, 4096)]
     my_rows = [sum(frames[u] for u in b) for b in batches]
@@ -994,6 +1008,11 @@ def main(argv=None):
     comm = torch.cuda.Stream() if gather else None
     checksum = torch.zeros((), dtype=torch.float64, device="cuda")
     reh = None
+    if args.rehearse_send and not args.rehearse_peers:
+        assert world == 1 and not gather, "--rehearse-send rehearses a sender in one process"
+        reh = {"stream": torch.cuda.Stream(), "done": [None] * nbuf, "recv": [],
+               "src": None, "acc": torch.zeros((), dtype=torch.float64, device="cuda"),
+               "part": torch.empty(gpu.SUM_PARTS, dtype=torch.float64, device="cuda")}
     if args.rehearse_peers:
         assert world == 1 and not gather, "--rehearse-peers rehearses rank 0 in one process"
         reh = {"stream": torch.cuda.Stream(), "done": [None] * nbuf,
@@ -1109,7 +1128,7 @@ def main(argv=None):
     share = 1.0
     if gather and rank == 0:
         share = args.sink_share if args.sink_share is not None else (
-            max(0.5, 1.0 - 0.054 * (world - 1)) if args.dist_backend == "nccl" else 1.0)
+            sink_share_default(world) if args.dist_backend == "nccl" else 1.0)
         assert 0.0 < share <= 1.0, "--sink-share must be in (0, 1]"
     elif reh is not None and args.sink_share is not None:
         share = args.sink_share  # the rehearsal of rank 0 at that share
@@ -1375,6 +1394,8 @@ def main(argv=None):
         line["verify"] = verify
         if verify_ranks is not None:
             line["verify_ranks"] = verify_ranks
+    if args.rehearse_send and not args.rehearse_peers:
+        line["rehearse_send"] = "every batch read once more after it is scored (a sender's local cost); measurement only"
     if args.rehearse_peers:
         line["rehearse_peers"] = {"peers": args.rehearse_peers,
                                   "what": "rank 0's receive copies and float64 folds of N = peers + 1 ranks, "

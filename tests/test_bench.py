@@ -120,3 +120,18 @@ def test_bench_world_size_mismatch_fails():
     assert r.returncode != 0
     assert "WORLD_SIZE 1" in r.stderr
     assert not _lines(r.stdout)
+
+
+def test_sink_share_default_balances_rank0_with_senders(bench):
+    """rank 0's rehearsed step (0.61 + 0.034 (N - 1) ms at a
+    full share, 0.71 ms per unit of share) is brought to a sender's 0.65-0.66
+    ms (profiles/r05z3_sender_rehearsal.txt); never below half a share."""
+    assert bench.sink_share_default(1) == 1.0
+    assert bench.sink_share_default(2) == 1.0
+    assert abs(bench.sink_share_default(8) - 0.681) < 1e-9
+    for n in range(2, 9):
+        f = bench.sink_share_default(n)
+        assert 0.5 <= f <= 1.0
+        rank0 = 0.61 + 0.034 * (n - 1) - 0.71 * (1.0 - f)
+        assert rank0 <= 0.67
+    assert bench.sink_share_default(64) == 0.5
