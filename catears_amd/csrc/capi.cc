@@ -1183,6 +1183,19 @@ static bool x6_first_direct() {
   return v && (x6_variant_env() == 0 || x6_variant_env() == 300);
 }
 
+// CATEARS_X6_CHAIN: the layers hand each other their outputs as bf16 planes
+// (the direct-weight kernel's OUT16 epilogue, read by its PIN loader), so
+// each activation is split once, in the epilogue that produces it, instead of
+// by every unit tile of the next layer that reads it.  Bit-identical to the
+// fp32 chain (tests/test_gpu_x6_variants.py).
+static bool x6_plane_chain_env() {
+  static const bool v = [] {
+    const char *e = getenv("CATEARS_X6_CHAIN");
+    return e && atoi(e) != 0;
+  }();
+  return v;
+}
+
 // CATEARS_LAT_FUSED_FINAL=0 keeps the last layer's split-K reduce as its own
 // launch before the finalize (bit-identical; the default fuses the two)
 static bool lat_fused_final() {
@@ -1198,7 +1211,15 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
   int max_in = 0;
   for (const Step &st : m->steps) max_in = std::max(max_in, st.gemm.kpad);
   for (const Step &st : m->steps) max_in = std::max(max_in, (st.gemm.n + 31) / 32 * 32);
-  const size_t blk = ((size_t)rows * max_in + 63) / 64 * 64;
+  // the plane chain: the first layer gathers the caller's fp32 rows in its
+  // loader, every layer has the fragment image, the later layers' segments
+  // are whole K-tiles
+  bool planes = x6_plane_chain_env() && !ctx->latency && x6_first_direct() && m->steps[0].gemm.din % 8 == 0 &&
+               ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+  for (size_t i = 0; planes && i < m->steps.size(); ++i)
+    planes = m->steps[i].gemm.wdir.ptr && (i == 0 || m->steps[i].gemm.din % 32 == 0);
+  // a block of planes is rows x 3 x width bf16: 1.5 floats per element
+  const size_t blk = ((size_t)rows * max_in * (planes ? 3 : 2) / 2 + 63) / 64 * 64;
   CE_TRY(ensure_workspace(ctx, 2 * blk + (size_t)rows * m->num_pdfs));
   float *buf[2] = {ctx->workspace.as<float>(), ctx->workspace.as<float>() + blk};
   float *out = ctx->workspace.as<float>() + 2 * blk;
@@ -1234,8 +1255,14 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
       a.nseg = g.nseg;
       for (int s = 0; s < 8; ++s) a.off[s] = g.off[s];
     }
-    a.xf = xs;
-    a.ldx = px;
+    if (planes && i > 0) {
+      a.x = reinterpret_cast<const uint16_t *>(xs);
+      a.ldx = 3 * px;
+      a.px = px;
+    } else {
+      a.xf = xs;
+      a.ldx = px;
+    }
     a.wf = g.wt.as<float>();
     a.ldw = g.kpad;
     a.w = g.wsplit.as<uint16_t>();  // the same weights as planes (kernels that read them)
@@ -1251,8 +1278,14 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
     for (int q = 0; q < 4; ++q) a.post[q] = g.post[q];
     a.npost = g.npost;
     const int pn = (g.n + 31) / 32 * 32;
-    a.y32 = last ? out : buf[cur];
-    a.ldy = last ? g.n : pn;
+    if (planes && !last) {
+      a.y16 = reinterpret_cast<uint16_t *>(buf[cur]);
+      a.ldy = 3 * pn;
+      a.py = pn;
+    } else {
+      a.y32 = last ? out : buf[cur];
+      a.ldy = last ? g.n : pn;
+    }
     {
       ProfScope prof(ctx, CE_GPU_PROF_GEMM);
       if (ctx->latency) {

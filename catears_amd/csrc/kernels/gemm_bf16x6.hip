@@ -668,12 +668,21 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
 // lives in sub-stage t & 1 of stage (t >> 1) & 1, tile t + 2 is split and
 // written during tile t and loaded during tile t - 1 (one tile more of load
 // slack).  Same products in the same order: bit-identical to KS = 1.
-template <class C, bool FIRST = false, int DIAG = 0, int KS = 1>
+// PIN / OUT16 (the plane chain, x6_plane_chain in capi.cc): the activations
+// arrive already split -- three bf16 planes per row, written once by the
+// previous layer's OUT16 epilogue -- so the loader moves three 16-byte plane
+// chunks per thread into LDS with no split VALU; OUT16 writes this layer's
+// output the same way for the next.  The planes are split3's, the loader's
+// split3_pair gives the same bits, so the chain is bit-identical to the fp32
+// chain.  Each activation is split once instead of once per unit tile that
+// reads it (4 per hidden layer, 14 for the output layer).
+template <class C, bool FIRST = false, int DIAG = 0, int KS = 1, bool PIN = false, bool OUT16 = false>
 __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
 #ifndef CATEARS_DIAG
   static_assert(DIAG == 0, "ablation builds (wrong results) only with -DCATEARS_DIAG");
 #endif
   static_assert(KS == 1 || (KS == 2 && !FIRST), "two K-tiles per stage: hidden layers only (even K-tile count)");
+  static_assert(!PIN || (!FIRST && KS == 1 && DIAG == 0), "plane input: hidden / output layers, one K-tile per stage");
   constexpr int BF = C::BF, TW = C::TW, TF = C::TF, NT = C::NT;
   constexpr int RPP = NT / 4;  // activation rows per pass (4 threads x 32 B per row)
   static_assert(BF == RPP, "one activation row chunk per thread");
@@ -688,6 +697,7 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   typedef const __attribute__((address_space(1))) f32x4v gvec;
   typedef const __attribute__((address_space(1))) bf16x8 gfrag;
+  typedef const __attribute__((address_space(1))) u32x4 gchunk;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ww = wave / C::WGF, wf = wave % C::WGF;
@@ -711,6 +721,7 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
     for (int i = 0; i < TW; ++i) dst[i] = wb[i][(kt * 3 + pl) * 64];
   };
   f32x4v rx0[2], rx1[2];  // activation row chunks of tiles kt+1 / kt+2 (by parity)
+  u32x4 rp[3][2];         // PIN: the three plane chunks of tiles kt+1 / kt+2
   // FIRST: every (segment, tile row)'s source row, gathered once into LDS
   // (a row_map load per K-tile would put a dependent global load in front of
   // every activation load; eight values in registers went to scratch)
@@ -740,6 +751,16 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
       rx0[r] = xb[0];
       rx1[r] = xb[1];
       if (seg >= p.nseg) rx0[r] = rx1[r] = f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+    } else if constexpr (PIN) {
+      // row src's 8 bf16 at k of each plane: element src * ldx + pl * px + k
+      const int seg = k0 / p.din, col0 = k0 - seg * p.din;
+      const int shift = (int)(signed char)(p.off_packed >> (8 * seg));
+      const int src = clampi(f0 + prow + shift, 0, p.m - 1);
+      const uint32_t o = ((uint32_t)(src * p.ldx) + col0 + 8 * pch) / 8, ps = (uint32_t)p.px / 8;
+      gchunk *xb = (gchunk *)p.x;
+      rp[0][r] = xb[o];
+      rp[1][r] = xb[o + ps];
+      rp[2][r] = xb[o + 2 * ps];
     } else {
       const int seg = k0 / p.din, col0 = k0 - seg * p.din;
       const int shift = (int)(signed char)(p.off_packed >> (8 * seg));
@@ -752,6 +773,12 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
   };
   auto put = [&](char *st, int r) {
     if constexpr ((DIAG & 2) != 0) return;
+    if constexpr (PIN) {
+      const int off = prow * 64 + ((pch ^ swz(prow)) * 16);
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<u32x4 *>(st + pl * BF * 64 + off) = rp[pl][r];
+      return;
+    }
     Planes2 q0, q1, q2, q3;
     if constexpr ((DIAG & 1) != 0) {
       auto raw = [](float a, float b) {
@@ -869,7 +896,7 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
   }
   if (KS == 1 && kt < ktiles) body(kt, std::integral_constant<int, 0>());
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the clamped tail prefetches
-  x6_epilogue<TW, TF, false>(p, acc, n0 + ww * TW * 16, f0 + frow, lane);
+  x6_epilogue<TW, TF, OUT16>(p, acc, n0 + ww * TW * 16, f0 + frow, lane);
 }
 
 #ifdef CATEARS_EXPERIMENTS
@@ -1200,9 +1227,20 @@ int launch_d(hipStream_t s, X6Args p) {
   p.tiles_n = (p.n + C::BW - 1) / C::BW;
   p.tiles_m = (p.m + C::BF - 1) / C::BF;
   dim3 grid(p.tiles_m * p.tiles_n), block(C::NT);
-  if (p.row_map || p.din % 32 != 0)  // the same rule as launch_gemm_bf16x6's `first`
-    hipLaunchKernelGGL((gemm_bf16x6d_kernel<C, true>), grid, block, 0, s, p);
-  else if (x6_ks() == 2 && (p.kpad / 32) % 2 == 0)
+  const bool out16 = p.y16 != nullptr;
+  if (p.row_map || p.din % 32 != 0) {  // the same rule as launch_gemm_bf16x6's `first`
+    if (out16)
+      hipLaunchKernelGGL((gemm_bf16x6d_kernel<C, true, 0, 1, false, true>), grid, block, 0, s, p);
+    else
+      hipLaunchKernelGGL((gemm_bf16x6d_kernel<C, true>), grid, block, 0, s, p);
+  } else if (!p.xf) {  // plane input (the plane chain)
+    if (out16)
+      hipLaunchKernelGGL((gemm_bf16x6d_kernel<C, false, 0, 1, true, true>), grid, block, 0, s, p);
+    else
+      hipLaunchKernelGGL((gemm_bf16x6d_kernel<C, false, 0, 1, true, false>), grid, block, 0, s, p);
+  } else if (out16) {  // fp32 input, planes out (a chain's whole-K-tile first layer)
+    hipLaunchKernelGGL((gemm_bf16x6d_kernel<C, false, 0, 1, false, true>), grid, block, 0, s, p);
+  } else if (x6_ks() == 2 && (p.kpad / 32) % 2 == 0)
     hipLaunchKernelGGL((gemm_bf16x6d_kernel<C, false, DIAG, 2>), grid, block, 0, s, p);
   else
     hipLaunchKernelGGL((gemm_bf16x6d_kernel<C, false, DIAG>), grid, block, 0, s, p);
@@ -1265,8 +1303,20 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
   if (a.n % 4 != 0 || a.ldy % 4 != 0 || (a.y16 && a.py % 4 != 0))
     return fail(CE_GPU_EINVAL, "gemm_bf16x6: output width must be a multiple of 4");
   const bool f32in = a.xf != nullptr;
+  // the plane chain (capi.cc x6_plane_chain): planes in and / or out of the
+  // direct-weight kernel
+  const bool direct = a.wd && (x6_variant() == 0 || x6_variant() == 300);
+  const bool pin = !f32in && a.x && a.wd;
+  if (pin) {
+    if (!direct || first || a.ldx % 8 || a.px % 8 || (reinterpret_cast<uintptr_t>(a.x) & 15) ||
+        (int64_t)a.m * a.ldx >= ((int64_t)1 << 31) || (int64_t)a.m * a.ldy >= ((int64_t)1 << 31))
+      return fail(CE_GPU_EINVAL, "gemm_bf16x6: plane input needs the direct-weight kernel, din % 32 == 0, "
+                                 "16-byte aligned planes and 2^31-element operands");
+  }
+  if (a.y16 && f32in && !direct)
+    return fail(CE_GPU_EINVAL, "gemm_bf16x6: fp32 input with split output needs the direct-weight kernel");
   if (f32in) {
-    if (!a.wf || !a.y32 || a.ldw % 4 || a.ldx % 4 || (reinterpret_cast<uintptr_t>(a.wf) & 15) ||
+    if (!a.wf || !(a.y32 || a.y16) || a.ldw % 4 || a.ldx % 4 || (reinterpret_cast<uintptr_t>(a.wf) & 15) ||
         (reinterpret_cast<uintptr_t>(a.xf) & 15))
       return fail(CE_GPU_EINVAL, "gemm_bf16x6: fp32 operands must be 16-byte aligned, output fp32");
     // the kernel forms row * ld element offsets in 32 bits
@@ -1323,6 +1373,12 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
   p.wd = a.wd;
   p.wd_kt = a.wd_kt;
   const bool out16 = a.y16 != nullptr;
+  if (pin || (f32in && out16)) {
+    if (a.wd_kt * 32 < a.kpad || (reinterpret_cast<uintptr_t>(a.wd) & 15))
+      return fail(CE_GPU_EINVAL, "gemm_bf16x6: weight fragment image does not cover K");
+    if (first && x6_first_tile() == 128) return launch_d<X6Cfg<128, 128, 2, 4, 2>>(s, p);
+    return launch_d<X6Cfg<kX6DirUnits, 128, 4, 2, 2>>(s, p);
+  }
   if (f32in) {
     switch (x6_variant()) {
       case 0:
@@ -1354,6 +1410,11 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
       case 302:  // direct weights, 128 x 128 tiles (twice the blocks of 300)
         if (!a.wd) return fail(CE_GPU_EINVAL, "variant 302 needs the weight fragment image");
         return launch_d<X6Cfg<128, 128, 2, 4, 2>>(s, p);
+      case 320:  // direct weights, 256 x 128 tiles as 8 waves of 32 units x 128 frames: no weight
+                 // fragment loaded by two waves (300: two waves along the frames share each)
+        if (!a.wd) return fail(CE_GPU_EINVAL, "variant 320 needs the weight fragment image");
+        if (first) return launch_d<X6Cfg<128, 128, 2, 4, 2>>(s, p);
+        return launch_d<X6Cfg<kX6DirUnits, 128, 8, 1, 2>>(s, p);
       case 42:  // round-1 default: split of tile kt+1, then the MFMAs of tile kt
         return launch_f<X6Cfg<128, 256, 2, 4, 2>>(s, p);
       case 55:  // MFMAs of tile kt first, the split interleaved by the compiler

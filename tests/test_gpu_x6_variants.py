@@ -58,6 +58,21 @@ def test_x6_variants_bit_identical(tmp_path, s_config):
     # two K-tiles per LDS stage against one (the default)
     ks2 = _run(0, s_config, tmp_path / "ks2.npy", CATEARS_X6_KS="2")
     assert np.array_equal(ks2, base), "two K-tiles per LDS stage differ from one"
+    # the plane chain: every layer's output split once, in its epilogue, and
+    # read as planes by the next (CATEARS_X6_CHAIN=1), on both first-layer
+    # tile widths
+    chain = _run(0, s_config, tmp_path / "chain.npy", CATEARS_X6_CHAIN="1")
+    assert np.array_equal(chain, base), "the plane chain differs from the fp32 chain"
+    chain256 = _run(0, s_config, tmp_path / "chain256.npy", CATEARS_X6_CHAIN="1", CATEARS_X6_FIRST_TILE="256")
+    assert np.array_equal(chain256, base), "the plane chain on 256-unit first-layer tiles differs"
+
+
+def test_x6_plane_chain_xs(tmp_path, xs_config):
+    """The plane chain on TDNN-XS (256-wide hidden layers, 512 pdfs: one
+    unit tile per layer, a partial last tile of the output layer)."""
+    base = _run(0, xs_config, tmp_path / "v0.npy")
+    chain = _run(0, xs_config, tmp_path / "chain.npy", CATEARS_X6_CHAIN="1")
+    assert np.array_equal(chain, base), "the plane chain differs from the fp32 chain on TDNN-XS"
 
 
 def test_unknown_variant_fails_loudly(tmp_path, s_config):
