@@ -676,7 +676,14 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
 // split3_pair gives the same bits, so the chain is bit-identical to the fp32
 // chain.  Each activation is split once instead of once per unit tile that
 // reads it (4 per hidden layer, 14 for the output layer).
-template <class C, bool FIRST = false, int DIAG = 0, int KS = 1, bool PIN = false, bool OUT16 = false>
+// PRIO: 1 (the default for hidden and output layers) raises the wave's issue
+// priority around its global load issues (s_setprio 1), so the other wave of
+// its SIMD does not hold them back behind an MFMA region: C3 +0.7-1.5 %,
+// alternating on two boxes (profiles/r05z8_x6_setprio.txt).  Experiment
+// builds: 0 none, 2 around the MFMA regions, 3 around the load issues and
+// LDS writes, 4 around the load issues and fragment reads (all equal or
+// below 1).  Priority changes issue order only: same bits.
+template <class C, bool FIRST = false, int DIAG = 0, int KS = 1, bool PIN = false, bool OUT16 = false, int PRIO = 0>
 __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
 #ifndef CATEARS_DIAG
   static_assert(DIAG == 0, "ablation builds (wrong results) only with -DCATEARS_DIAG");
@@ -837,22 +844,33 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
     // activation tile shares the 48-MFMA region so it interleaves.
     // Activation registers alternate by tile parity: tile kt+1's chunk
     // (loaded one tile ago) is written while tile kt+2's is loaded.
+    if constexpr (PRIO == 4) __builtin_amdgcn_s_setprio(1);
     read_b(st, 0, b0);
     read_b(st, 1, b1);
+    if constexpr (PRIO == 4) __builtin_amdgcn_s_setprio(0);
+    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4) __builtin_amdgcn_s_setprio(1);
     load_w(kt + 1, 0, a0[c ^ 1]);
+    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(1);
     if constexpr ((DIAG & 32) == 0) {
 #pragma unroll
       for (int i = 0; i < TW; ++i)
 #pragma unroll
         for (int j = 0; j < TF; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[c][i], b0[j], acc[i][j], 0, 0, 0);
     }
+    if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     // KS 1: load tile kt + 2 into rx[c], write tile kt + 1 from rx[c ^ 1];
     // KS 2: load tile kt + 3 into rx[c ^ 1], write tile kt + 2 from rx[c]
+    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4) __builtin_amdgcn_s_setprio(1);
     load_x(kt + KS + 1, KS == 1 ? c : c ^ 1);
+    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(1);
+    if constexpr (PRIO == 3) __builtin_amdgcn_s_setprio(1);
     put(sn, KS == 1 ? c ^ 1 : c);
+    if constexpr (PRIO == 3) __builtin_amdgcn_s_setprio(0);
     if constexpr ((DIAG & 32) == 0) {
 #pragma unroll
       for (int i = 0; i < TW; ++i)
@@ -863,10 +881,16 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b1[j], acc[i][j], 0, 0, 0);
         }
     }
+    if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(0);
+    if constexpr (PRIO == 4) __builtin_amdgcn_s_setprio(1);
     read_b(st, 2, b2);
+    if constexpr (PRIO == 4) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4) __builtin_amdgcn_s_setprio(1);
     load_w(kt + 1, 1, a1);
+    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(1);
     if constexpr ((DIAG & 32) == 0) {
 #pragma unroll
       for (int i = 0; i < TW; ++i)
@@ -881,8 +905,11 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
       for (int j = 0; j < TF; ++j) acc[0][j][0] += (float)b0[j][0] + (float)b1[j][0] + (float)b2[j][0] +
                                                    (float)a0[c][0][0] + (float)a1[0][0] + (float)a2[0][0];
     }
+    if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4) __builtin_amdgcn_s_setprio(1);
     load_w(kt + 1, 2, a2);
+    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4) __builtin_amdgcn_s_setprio(0);
     if constexpr (KS == 1 || c == 1) {  // KS 2: once per stage (after its odd tile)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if constexpr ((DIAG & 16) == 0) __builtin_amdgcn_s_barrier();
@@ -1222,7 +1249,7 @@ int x6_ks() {
   return v;
 }
 
-template <class C, int DIAG = 0>
+template <class C, int DIAG = 0, int PRIO = 1>
 int launch_d(hipStream_t s, X6Args p) {
   p.tiles_n = (p.n + C::BW - 1) / C::BW;
   p.tiles_m = (p.m + C::BF - 1) / C::BF;
@@ -1243,7 +1270,7 @@ int launch_d(hipStream_t s, X6Args p) {
   } else if (x6_ks() == 2 && (p.kpad / 32) % 2 == 0)
     hipLaunchKernelGGL((gemm_bf16x6d_kernel<C, false, DIAG, 2>), grid, block, 0, s, p);
   else
-    hipLaunchKernelGGL((gemm_bf16x6d_kernel<C, false, DIAG>), grid, block, 0, s, p);
+    hipLaunchKernelGGL((gemm_bf16x6d_kernel<C, false, DIAG, 1, false, false, PRIO>), grid, block, 0, s, p);
   CE_HIP(hipGetLastError());
   return CE_GPU_OK;
 }
@@ -1415,6 +1442,16 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
         if (!a.wd) return fail(CE_GPU_EINVAL, "variant 320 needs the weight fragment image");
         if (first) return launch_d<X6Cfg<128, 128, 2, 4, 2>>(s, p);
         return launch_d<X6Cfg<kX6DirUnits, 128, 8, 1, 2>>(s, p);
+      case 330:  // 300 without the load-issue priority (the round-5 default before it)
+      case 332:  // 300 with s_setprio 1 around the MFMA regions instead
+      case 333:  // ... around the load issues and the LDS writes
+      case 334:  // ... around the load issues and the fragment reads
+        if (!a.wd) return fail(CE_GPU_EINVAL, "variants 330-334 need the weight fragment image");
+        if (first) return launch_d<X6Cfg<128, 128, 2, 4, 2>>(s, p);
+        if (x6_variant() == 330) return launch_d<X6Cfg<kX6DirUnits, 128, 4, 2, 2>, 0, 0>(s, p);
+        if (x6_variant() == 333) return launch_d<X6Cfg<kX6DirUnits, 128, 4, 2, 2>, 0, 3>(s, p);
+        if (x6_variant() == 334) return launch_d<X6Cfg<kX6DirUnits, 128, 4, 2, 2>, 0, 4>(s, p);
+        return launch_d<X6Cfg<kX6DirUnits, 128, 4, 2, 2>, 0, 2>(s, p);
       case 42:  // round-1 default: split of tile kt+1, then the MFMAs of tile kt
         return launch_f<X6Cfg<128, 256, 2, 4, 2>>(s, p);
       case 55:  // MFMAs of tile kt first, the split interleaved by the compiler
