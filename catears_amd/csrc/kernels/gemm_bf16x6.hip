@@ -676,13 +676,12 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
 // split3_pair gives the same bits, so the chain is bit-identical to the fp32
 // chain.  Each activation is split once instead of once per unit tile that
 // reads it (4 per hidden layer, 14 for the output layer).
-// PRIO: 1 (the default for hidden and output layers) raises the wave's issue
-// priority around its global load issues (s_setprio 1), so the other wave of
-// its SIMD does not hold them back behind an MFMA region: C3 +0.7-1.5 %,
-// alternating on two boxes (profiles/r05z8_x6_setprio.txt).  Experiment
-// builds: 0 none, 2 around the MFMA regions, 3 around the load issues and
-// LDS writes, 4 around the load issues and fragment reads (all equal or
-// below 1).  Priority changes issue order only: same bits.
+// PRIO (experiment builds; the product runs 0): 1 raises the wave's issue
+// priority around its global load issues (s_setprio 1), 2 around its MFMA
+// regions, 3 around the load issues and LDS writes, 4 around the load issues
+// and fragment reads, 5 as 1 with the activation loads issued at the top of
+// the K-tile.  None is faster than 0 once the run order is balanced
+// (profiles/r05z8_x6_setprio.txt).  Same bits.
 template <class C, bool FIRST = false, int DIAG = 0, int KS = 1, bool PIN = false, bool OUT16 = false, int PRIO = 0>
 __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
 #ifndef CATEARS_DIAG
@@ -848,9 +847,10 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
     read_b(st, 0, b0);
     read_b(st, 1, b1);
     if constexpr (PRIO == 4) __builtin_amdgcn_s_setprio(0);
-    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4) __builtin_amdgcn_s_setprio(1);
+    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4 || PRIO == 5) __builtin_amdgcn_s_setprio(1);
     load_w(kt + 1, 0, a0[c ^ 1]);
-    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4) __builtin_amdgcn_s_setprio(0);
+    if constexpr (PRIO == 5) load_x(kt + KS + 1, KS == 1 ? c : c ^ 1);  // activations issued first thing
+    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4 || PRIO == 5) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(1);
     if constexpr ((DIAG & 32) == 0) {
@@ -863,9 +863,9 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
     __builtin_amdgcn_sched_barrier(0);
     // KS 1: load tile kt + 2 into rx[c], write tile kt + 1 from rx[c ^ 1];
     // KS 2: load tile kt + 3 into rx[c ^ 1], write tile kt + 2 from rx[c]
-    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4) __builtin_amdgcn_s_setprio(1);
-    load_x(kt + KS + 1, KS == 1 ? c : c ^ 1);
-    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4) __builtin_amdgcn_s_setprio(0);
+    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4 || PRIO == 5) __builtin_amdgcn_s_setprio(1);
+    if constexpr (PRIO != 5) load_x(kt + KS + 1, KS == 1 ? c : c ^ 1);
+    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4 || PRIO == 5) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(1);
     if constexpr (PRIO == 3) __builtin_amdgcn_s_setprio(1);
@@ -886,9 +886,9 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
     read_b(st, 2, b2);
     if constexpr (PRIO == 4) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4) __builtin_amdgcn_s_setprio(1);
+    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4 || PRIO == 5) __builtin_amdgcn_s_setprio(1);
     load_w(kt + 1, 1, a1);
-    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4) __builtin_amdgcn_s_setprio(0);
+    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4 || PRIO == 5) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(1);
     if constexpr ((DIAG & 32) == 0) {
@@ -907,9 +907,9 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
     }
     if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4) __builtin_amdgcn_s_setprio(1);
+    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4 || PRIO == 5) __builtin_amdgcn_s_setprio(1);
     load_w(kt + 1, 2, a2);
-    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4) __builtin_amdgcn_s_setprio(0);
+    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4 || PRIO == 5) __builtin_amdgcn_s_setprio(0);
     if constexpr (KS == 1 || c == 1) {  // KS 2: once per stage (after its odd tile)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if constexpr ((DIAG & 16) == 0) __builtin_amdgcn_s_barrier();
@@ -1249,7 +1249,7 @@ int x6_ks() {
   return v;
 }
 
-template <class C, int DIAG = 0, int PRIO = 1>
+template <class C, int DIAG = 0, int PRIO = 0>
 int launch_d(hipStream_t s, X6Args p) {
   p.tiles_n = (p.n + C::BW - 1) / C::BW;
   p.tiles_m = (p.m + C::BF - 1) / C::BF;
@@ -1442,15 +1442,17 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
         if (!a.wd) return fail(CE_GPU_EINVAL, "variant 320 needs the weight fragment image");
         if (first) return launch_d<X6Cfg<128, 128, 2, 4, 2>>(s, p);
         return launch_d<X6Cfg<kX6DirUnits, 128, 8, 1, 2>>(s, p);
-      case 330:  // 300 without the load-issue priority (the round-5 default before it)
-      case 332:  // 300 with s_setprio 1 around the MFMA regions instead
+      case 331:  // 300 with s_setprio 1 around the load issues
+      case 332:  // 300 with s_setprio 1 around the MFMA regions
       case 333:  // ... around the load issues and the LDS writes
       case 334:  // ... around the load issues and the fragment reads
-        if (!a.wd) return fail(CE_GPU_EINVAL, "variants 330-334 need the weight fragment image");
+      case 335:  // the default's priority, activation loads issued at the top of the K-tile
+        if (!a.wd) return fail(CE_GPU_EINVAL, "variants 331-335 need the weight fragment image");
         if (first) return launch_d<X6Cfg<128, 128, 2, 4, 2>>(s, p);
-        if (x6_variant() == 330) return launch_d<X6Cfg<kX6DirUnits, 128, 4, 2, 2>, 0, 0>(s, p);
+        if (x6_variant() == 331) return launch_d<X6Cfg<kX6DirUnits, 128, 4, 2, 2>, 0, 1>(s, p);
         if (x6_variant() == 333) return launch_d<X6Cfg<kX6DirUnits, 128, 4, 2, 2>, 0, 3>(s, p);
         if (x6_variant() == 334) return launch_d<X6Cfg<kX6DirUnits, 128, 4, 2, 2>, 0, 4>(s, p);
+        if (x6_variant() == 335) return launch_d<X6Cfg<kX6DirUnits, 128, 4, 2, 2>, 0, 5>(s, p);
         return launch_d<X6Cfg<kX6DirUnits, 128, 4, 2, 2>, 0, 2>(s, p);
       case 42:  // round-1 default: split of tile kt+1, then the MFMAs of tile kt
         return launch_f<X6Cfg<128, 256, 2, 4, 2>>(s, p);
