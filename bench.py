@@ -42,6 +42,9 @@ FLOPS_PER_FRAME_FAST = FLOPS_PER_FRAME - 2 * 200 * 1024
 MFMA_F32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: dense fp32 MFMA (= vector) peak
 MFMA_I8_PEAK_TOPS = 5000.0       # MI355X_MICROARCH.md: int8 MFMA = 2x the ~2.5 PF dense bf16 rate
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: ~2.5 PF dense bf16 / fp16 (no sparsity)
+# measured: v_mfma_f32_16x16x32_bf16 sustained on the whole chip with changing operands, at the
+# socket power cap (profiles/r05z10_mfma_power.txt, tools/probes/mfma_power_probe.hip)
+MFMA_BF16_SUSTAINED_TFLOPS = 1966.0
 # Split-plane GEMMs (ce_gpu_model_set_gemm): bf16x6 issues six bf16 MFMA
 # products per fp32 multiply-add, f16x3 three fp16 ones, so the kernel's
 # ceiling in fp32 (algorithmic) FLOP/s is the 16-bit dense peak / products.
@@ -1297,6 +1300,8 @@ def main(argv=None):
                                       "multiply-add (achieved = fp32 algorithmic FLOPs)",
                         "mfma_16bit_tflops": round(achieved * prods, 1),
                         "vs_fp32_mfma_peak": round(achieved / MFMA_F32_PEAK_TFLOPS, 4),
+                        # the same work against the bf16 rate the chip sustains at its power cap
+                        "frac_of_sustained_mfma": round(achieved * prods / MFMA_BF16_SUSTAINED_TFLOPS, 4),
                         "traffic": traffic, "traffic_source": src,
                         "kernel": kname + (" (every TDNN-S Linear, layers 1-7; rocprof: tools/trace_summary.py)"
                                            if f32in else " + its fp32-output form (TDNN-S layers 1-7; rocprof: "
