@@ -120,6 +120,10 @@ def parse(argv=None):
                          "the library's (bf16x6: three exact bf16 planes, six products, fp32 GEMM)")
     ap.add_argument("--front-streams", type=int, default=1,
                     help="fbank + CMVN streams; consecutive batches alternate between them")
+    ap.add_argument("--wide-tiles", choices=["none", "last", "ends"], default="none",
+                    help="c3: score the last (or the first and the last) batch of each run of steps on 128 x 128 "
+                         "bf16x6 tiles (ce_gpu_ctx_set_wide_tiles: all CUs per launch while the pipeline fills or "
+                         "drains); same bits")
     ap.add_argument("--sink-share", type=float, default=None,
                     help="c3 / c4, N > 1: the fraction of steps (c4: of the corpus share) rank 0 scores a batch "
                          "of its own (it also receives and folds every peer's rows).  Default on RCCL: "
@@ -1152,6 +1156,9 @@ def main(argv=None):
 
     def run(first, count):
         todo = [i for i in range(first, first + count) if scores(i)]
+        wide = set()
+        if todo and args.wide_tiles != "none":
+            wide = {todo[-1]} | ({todo[0]} if args.wide_tiles == "ends" else set())
         if todo:
             front_stage(todo[0])
         k = 0
@@ -1165,7 +1172,11 @@ def main(argv=None):
                 continue
             if k + 1 < len(todo):
                 front_stage(todo[k + 1])
+            if i in wide:
+                ctxs[i % NB].set_wide_tiles(True)
             back_stage(i)
+            if i in wide:
+                ctxs[i % NB].set_wide_tiles(False)
             k += 1
 
     # pre-warm: the same steps, nothing gathered, dumped or folded, until the
@@ -1399,6 +1410,10 @@ def main(argv=None):
         line["verify"] = verify
         if verify_ranks is not None:
             line["verify_ranks"] = verify_ranks
+    if args.wide_tiles != "none":
+        line["config"]["wide_tiles"] = {"last": "the last batch of each run of steps",
+                                        "ends": "the first and the last batch of each run of steps"}[
+            args.wide_tiles] + " on 128 x 128 bf16x6 tiles (ce_gpu_ctx_set_wide_tiles, same bits)"
     if args.rehearse_send and not args.rehearse_peers:
         line["rehearse_send"] = "every batch read once more after it is scored (a sender's local cost); measurement only"
     if args.rehearse_peers:

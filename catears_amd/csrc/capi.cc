@@ -745,6 +745,12 @@ int ce_gpu_ctx_set_latency(ce_gpu_ctx *ctx, int on) {
   return CE_GPU_OK;
 }
 
+int ce_gpu_ctx_set_wide_tiles(ce_gpu_ctx *ctx, int on) {
+  if (!ctx) return fail(CE_GPU_EINVAL, "NULL argument");
+  ctx->wide_tiles = on ? 1 : 0;
+  return CE_GPU_OK;
+}
+
 int ce_gpu_ctx_set_fbank(ce_gpu_ctx *ctx, int mode) {
   if (!ctx) return fail(CE_GPU_EINVAL, "NULL argument");
   if (mode != CE_GPU_FBANK_EXACT && mode != CE_GPU_FBANK_FAST) return fail(CE_GPU_EINVAL, "unknown fbank mode");
@@ -1269,6 +1275,7 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
     a.pw = g.kpad;
     a.wd = g.wdir.as<uint16_t>();   // and as MFMA fragments (the default kernel)
     a.wd_kt = g.kpad / 32;
+    a.wide = ctx->wide_tiles != 0;
     a.m = rows;
     a.n = g.n;
     a.kpad = i == 0 ? g.kpad : g.nseg * g.din;

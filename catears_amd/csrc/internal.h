@@ -288,6 +288,9 @@ struct X6Gemm {
   // latency kernel: leave the last layer's slice reduce to
   // launch_lat_finalize (described in *tail) when it can run there
   struct LatTail *tail = nullptr;
+  // ce_gpu_ctx_set_wide_tiles: the direct-weight kernel on 128 x 128 tiles
+  // for every layer (twice the blocks of the 256 x 128 default)
+  bool wide = false;
 };
 
 // The last layer's slice partials when its reduce runs inside the finalize
@@ -318,6 +321,7 @@ struct ce_gpu_ctx {
   catears::DevBuf overflow;    // int: an f16x3 split left the fp16 range (ce_gpu_ctx_overflow)
   catears::DevBuf lat_part;    // latency GEMM: slice partials (grown on demand)
   int latency = 0;             // ce_gpu_ctx_set_latency: split-K GEMMs for small batches
+  int wide_tiles = 0;          // ce_gpu_ctx_set_wide_tiles: 128 x 128 bf16x6 tiles (all CUs per launch)
   int fbank_mode = 0;          // ce_gpu_ctx_set_fbank: CE_GPU_FBANK_EXACT / _FAST
   std::vector<int32_t> h_blk_maps;
   // optional per-class launch timing (ce_gpu_ctx_profile)

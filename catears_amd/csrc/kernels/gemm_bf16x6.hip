@@ -1403,7 +1403,7 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
   if (pin || (f32in && out16)) {
     if (a.wd_kt * 32 < a.kpad || (reinterpret_cast<uintptr_t>(a.wd) & 15))
       return fail(CE_GPU_EINVAL, "gemm_bf16x6: weight fragment image does not cover K");
-    if (first && x6_first_tile() == 128) return launch_d<X6Cfg<128, 128, 2, 4, 2>>(s, p);
+    if (a.wide || (first && x6_first_tile() == 128)) return launch_d<X6Cfg<128, 128, 2, 4, 2>>(s, p);
     return launch_d<X6Cfg<kX6DirUnits, 128, 4, 2, 2>>(s, p);
   }
   if (f32in) {
@@ -1414,8 +1414,10 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
           if (a.wd_kt * 32 < a.kpad || (reinterpret_cast<uintptr_t>(a.wd) & 15))
             return fail(CE_GPU_EINVAL, "gemm_bf16x6: weight fragment image does not cover K");
           // the gathered first layer (K of a few tiles: prologue and
-          // epilogue bound) on 128 x 128 tiles -- twice the blocks
-          if (first && x6_first_tile() == 128) return launch_d<X6Cfg<128, 128, 2, 4, 2>>(s, p);
+          // epilogue bound) on 128 x 128 tiles -- twice the blocks; every
+          // layer so with ce_gpu_ctx_set_wide_tiles (a batch scored while
+          // no other is in flight then fills all CUs)
+          if (a.wide || (first && x6_first_tile() == 128)) return launch_d<X6Cfg<128, 128, 2, 4, 2>>(s, p);
           return launch_d<X6Cfg<kX6DirUnits, 128, 4, 2, 2>>(s, p);
         }
         [[fallthrough]];

@@ -31,7 +31,7 @@ ABI = [
     "ce_gpu_profile_anchor", "ce_gpu_ctx_profile_intervals", "ce_gpu_model_quantize",
     "ce_gpu_nnet_propagate_blocks", "ce_gpu_loglik_gather", "ce_gpu_loglik_columns",
     "ce_gpu_model_set_gemm", "ce_gpu_model_get_gemm", "ce_gpu_ctx_overflow", "ce_gpu_ctx_set_latency",
-    "ce_gpu_fbank_s16", "ce_gpu_score_s16", "ce_gpu_ctx_set_fbank", "ce_gpu_sum_f64",
+    "ce_gpu_fbank_s16", "ce_gpu_score_s16", "ce_gpu_ctx_set_fbank", "ce_gpu_sum_f64", "ce_gpu_ctx_set_wide_tiles",
     "ce_gpu_sum_f64_many",
 ]
 
@@ -104,6 +104,7 @@ def lib():
         "ce_gpu_ctx_overflow": (ci, [vp, pi]),
         "ce_gpu_ctx_set_latency": (ci, [vp, ci]),
         "ce_gpu_ctx_set_fbank": (ci, [vp, ci]),
+        "ce_gpu_ctx_set_wide_tiles": (ci, [vp, ci]),
         "ce_gpu_sum_f64": (ci, [vp, vp, i64, vp, vp]),
         "ce_gpu_sum_f64_many": (ci, [vp, ci, ctypes.POINTER(vp), pi64, vp, vp]),
     }
@@ -155,6 +156,12 @@ class Context:
         check(lib().ce_gpu_ctx_set_latency(self.h, int(bool(on))))
 
     FBANK_MODES = {"exact": 0, "fast": 1}
+
+    def set_wide_tiles(self, on=True):
+        """128 x 128 bf16x6 tiles for every layer (ce_gpu_ctx_set_wide_tiles):
+        all CUs per launch, for a batch scored while no other is in flight.
+        Same bits as the default tiles."""
+        check(lib().ce_gpu_ctx_set_wide_tiles(self.h, int(bool(on))))
 
     def set_fbank(self, mode="exact"):
         """Fbank kernel of this context (ce_gpu_ctx_set_fbank): "exact" (the

@@ -104,6 +104,16 @@ int ce_gpu_ctx_overflow(ce_gpu_ctx *ctx, int *overflow);
  * throughput mode for full 4096-row batches. */
 int ce_gpu_ctx_set_latency(ce_gpu_ctx *ctx, int on);
 
+/* Tile shape of ctx's throughput-mode bf16x6 GEMMs (round 5): on (1), every
+ * layer runs the direct-weight kernel on 128 x 128 tiles -- twice the blocks
+ * of the 256 x 128 default, so a hidden layer of a 4072-row batch fills all
+ * 256 CUs (140 vs 202 us alone) at 38 % more CU time.  For a batch scored
+ * while no other is in flight (a pipeline's first and last, or one batch on
+ * an idle GPU); the default suits batches that share the chip.  Same bits
+ * either way (tests/test_gpu_x6_variants.py).  Replaces nothing in the
+ * reference (a scheduling choice of this implementation). */
+int ce_gpu_ctx_set_wide_tiles(ce_gpu_ctx *ctx, int on);
+
 /* Fbank kernel of ctx's ce_gpu_fbank / ce_gpu_fbank_s16 / ce_gpu_score*:
  *   CE_GPU_FBANK_EXACT (default) the reference's operation order
  *       (src/fbank.cc:44-245, src/srfft.cc:124-459): pre-log mel energies

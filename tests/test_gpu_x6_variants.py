@@ -21,6 +21,8 @@ CHILD = r"""
 import sys, numpy as np, torch
 from catears_amd import gpu
 ctx = gpu.Context(0)
+if len(sys.argv) > 3 and sys.argv[3] == "wide":
+    ctx.set_wide_tiles(True)
 model = gpu.Model(ctx, sys.argv[1])
 assert model.gemm == "bf16x6", model.gemm
 x = np.random.default_rng(750).normal(9.0, 3.0, size=(3000, 40)).astype(np.float32)
@@ -29,15 +31,15 @@ np.save(sys.argv[2], out)
 """
 
 
-def _child(variant, cfg, path, **extra_env):
+def _child(variant, cfg, path, *args, **extra_env):
     env = dict(os.environ, CATEARS_X6_VARIANT=str(variant), PYTHONPATH=ROOT, **extra_env)
     env.pop("CATEARS_HIP_LIB", None)
-    return subprocess.run([sys.executable, "-c", CHILD, cfg, str(path)], env=env, capture_output=True, text=True,
-                          timeout=300, cwd=ROOT)
+    return subprocess.run([sys.executable, "-c", CHILD, cfg, str(path), *args], env=env, capture_output=True,
+                          text=True, timeout=300, cwd=ROOT)
 
 
-def _run(variant, cfg, path, **extra_env):
-    r = _child(variant, cfg, path, **extra_env)
+def _run(variant, cfg, path, *args, **extra_env):
+    r = _child(variant, cfg, path, *args, **extra_env)
     assert r.returncode == 0, r.stderr[-3000:]
     return np.load(path).view(np.uint32)
 
@@ -65,6 +67,9 @@ def test_x6_variants_bit_identical(tmp_path, s_config):
     assert np.array_equal(chain, base), "the plane chain differs from the fp32 chain"
     chain256 = _run(0, s_config, tmp_path / "chain256.npy", CATEARS_X6_CHAIN="1", CATEARS_X6_FIRST_TILE="256")
     assert np.array_equal(chain256, base), "the plane chain on 256-unit first-layer tiles differs"
+    # every layer on 128 x 128 tiles (ce_gpu_ctx_set_wide_tiles)
+    wide = _run(0, s_config, tmp_path / "wide.npy", "wide")
+    assert np.array_equal(wide, base), "128 x 128 tiles (wide) differ from the default tiles"
 
 
 def test_x6_plane_chain_xs(tmp_path, xs_config):
