@@ -683,7 +683,7 @@ __global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6f_kernel(X6Args p) {
 // the K-tile.  None is faster than 0 once the run order is balanced
 // (profiles/r05z8_x6_setprio.txt).  Same bits.
 template <class C, bool FIRST = false, int DIAG = 0, int KS = 1, bool PIN = false, bool OUT16 = false, int PRIO = 0>
-__global__ __launch_bounds__(C::NT, 1) void gemm_bf16x6d_kernel(X6Args p) {
+__global__ __launch_bounds__(C::NT, 512 / C::NT) void gemm_bf16x6d_kernel(X6Args p) {  // 8 waves per CU
 #ifndef CATEARS_DIAG
   static_assert(DIAG == 0, "ablation builds (wrong results) only with -DCATEARS_DIAG");
 #endif
@@ -1444,6 +1444,11 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
         if (!a.wd) return fail(CE_GPU_EINVAL, "variant 320 needs the weight fragment image");
         if (first) return launch_d<X6Cfg<128, 128, 2, 4, 2>>(s, p);
         return launch_d<X6Cfg<kX6DirUnits, 128, 8, 1, 2>>(s, p);
+      case 340:  // direct weights, 256 x 64 tiles of 4 waves (64 x 64 each): two blocks per CU,
+                 // barriers over four waves instead of eight
+        if (!a.wd) return fail(CE_GPU_EINVAL, "variant 340 needs the weight fragment image");
+        if (first) return launch_d<X6Cfg<128, 128, 2, 4, 2>>(s, p);
+        return launch_d<X6Cfg<kX6DirUnits, 64, 4, 1, 2>>(s, p);
       case 331:  // 300 with s_setprio 1 around the load issues
       case 332:  // 300 with s_setprio 1 around the MFMA regions
       case 333:  // ... around the load issues and the LDS writes
