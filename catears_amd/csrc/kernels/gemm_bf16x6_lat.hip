@@ -380,10 +380,22 @@ void launch_lat_gemm(hipStream_t s, LatArgs p) {
 
 }  // namespace
 
+// CATEARS_LAT_TARGET (measurement knob): the blocks per row tile the slice
+// rule aims at (default kLatTarget); fewer means fewer, longer slices and a
+// shorter reduce.  Other values change the fp32 summation order.
+static int lat_target() {
+  static const int v = [] {
+    const char *e = getenv("CATEARS_LAT_TARGET");
+    const int t = e ? atoi(e) : 0;
+    return t > 0 ? t : kLatTarget;
+  }();
+  return v;
+}
+
 int x6_lat_slices(int kpad, int n) {
   const int ktiles = kpad / 32, cols = (n + kLatBW - 1) / kLatBW;
-  // at most kLatTarget blocks per row tile (one wave of blocks over the CUs)
-  int slices = std::max(1, std::min(ktiles, kLatTarget / cols));
+  // at most lat_target() blocks per row tile (one wave of blocks over the CUs)
+  int slices = std::max(1, std::min(ktiles, lat_target() / cols));
   int per = (ktiles + slices - 1) / slices;
   per = std::min(per, kLatMaxKt);
   return (ktiles + per - 1) / per;  // no empty slice
