@@ -380,16 +380,20 @@ void launch_lat_gemm(hipStream_t s, LatArgs p) {
 
 }  // namespace
 
-// CATEARS_LAT_TARGET (measurement knob): the blocks per row tile the slice
-// rule aims at (default kLatTarget); fewer means fewer, longer slices and a
-// shorter reduce.  Other values change the fp32 summation order.
+// CATEARS_LAT_TARGET (experiments library only, tools/experiments/gpu_r5z16.sh):
+// the blocks per row tile the slice rule aims at (default kLatTarget); other
+// values change the fp32 summation order, so the product library ignores it.
 static int lat_target() {
+#ifdef CATEARS_EXPERIMENTS
   static const int v = [] {
     const char *e = getenv("CATEARS_LAT_TARGET");
     const int t = e ? atoi(e) : 0;
     return t > 0 ? t : kLatTarget;
   }();
   return v;
+#else
+  return kLatTarget;
+#endif
 }
 
 int x6_lat_slices(int kpad, int n) {
