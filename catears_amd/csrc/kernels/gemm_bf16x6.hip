@@ -48,6 +48,10 @@
 #include "../internal.h"
 #include "../tile_order.h"
 
+#ifndef CATEARS_X6_NT
+#define CATEARS_X6_NT 0
+#endif
+
 namespace catears {
 namespace {
 
@@ -168,7 +172,12 @@ __device__ __forceinline__ void x6_epilogue(const X6Args &p, const f32x4 (&acc)[
           *reinterpret_cast<u16x4 *>(dst + p.py) = u16x4{m[0], m[1], m[2], m[3]};
           *reinterpret_cast<u16x4 *>(dst + 2 * p.py) = u16x4{l[0], l[1], l[2], l[3]};
         } else {
+#if CATEARS_X6_NT
+          // measurement build (X6FLAGS=-DCATEARS_X6_NT=1): non-temporal output stores
+          __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(p.y32 + (int64_t)f * p.ldy + n));
+#else
           *reinterpret_cast<f32x4 *>(p.y32 + (int64_t)f * p.ldy + n) = v;
+#endif
         }
       }
     }
