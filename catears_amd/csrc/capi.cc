@@ -1194,10 +1194,12 @@ static bool x6_first_direct() {
 // each activation is split once, in the epilogue that produces it, instead of
 // by every unit tile of the next layer that reads it.  Bit-identical to the
 // fp32 chain (tests/test_gpu_x6_variants.py).
-static bool x6_plane_chain_env() {
-  static const bool v = [] {
+// 2: only the output layer reads planes (its 14 unit tiles would each split
+// the same activations), written by the layer before it.
+static int x6_plane_chain_env() {
+  static const int v = [] {
     const char *e = getenv("CATEARS_X6_CHAIN");
-    return e && atoi(e) != 0;
+    return e ? atoi(e) : 0;
   }();
   return v;
 }
@@ -1220,7 +1222,8 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
   // the plane chain: the first layer gathers the caller's fp32 rows in its
   // loader, every layer has the fragment image, the later layers' segments
   // are whole K-tiles
-  bool planes = x6_plane_chain_env() && !ctx->latency && x6_first_direct() && m->steps[0].gemm.din % 8 == 0 &&
+  const int chain_mode = x6_plane_chain_env();
+  bool planes = chain_mode != 0 && !ctx->latency && x6_first_direct() && m->steps[0].gemm.din % 8 == 0 &&
                ldx % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
   for (size_t i = 0; planes && i < m->steps.size(); ++i)
     planes = m->steps[i].gemm.wdir.ptr && (i == 0 || m->steps[i].gemm.din % 32 == 0);
@@ -1261,7 +1264,12 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
       a.nseg = g.nseg;
       for (int s = 0; s < 8; ++s) a.off[s] = g.off[s];
     }
-    if (planes && i > 0) {
+    // planes into layer i / out of it: every layer after the first (mode 1),
+    // or the output layer only (mode 2)
+    const size_t nst = m->steps.size();
+    const bool pin = planes && i > 0 && (chain_mode != 2 || i + 1 == nst);
+    const bool pout = planes && !last && (chain_mode != 2 || i + 2 == nst);
+    if (pin) {
       a.x = reinterpret_cast<const uint16_t *>(xs);
       a.ldx = 3 * px;
       a.px = px;
@@ -1285,7 +1293,7 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
     for (int q = 0; q < 4; ++q) a.post[q] = g.post[q];
     a.npost = g.npost;
     const int pn = (g.n + 31) / 32 * 32;
-    if (planes && !last) {
+    if (pout) {
       a.y16 = reinterpret_cast<uint16_t *>(buf[cur]);
       a.ldy = 3 * pn;
       a.py = pn;

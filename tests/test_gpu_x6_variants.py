@@ -67,6 +67,9 @@ def test_x6_variants_bit_identical(tmp_path, s_config):
     assert np.array_equal(chain, base), "the plane chain differs from the fp32 chain"
     chain256 = _run(0, s_config, tmp_path / "chain256.npy", CATEARS_X6_CHAIN="1", CATEARS_X6_FIRST_TILE="256")
     assert np.array_equal(chain256, base), "the plane chain on 256-unit first-layer tiles differs"
+    # planes into the output layer only (CATEARS_X6_CHAIN=2)
+    last = _run(0, s_config, tmp_path / "chain2.npy", CATEARS_X6_CHAIN="2")
+    assert np.array_equal(last, base), "planes into the output layer only differ"
     # every layer on 128 x 128 tiles (ce_gpu_ctx_set_wide_tiles)
     wide = _run(0, s_config, tmp_path / "wide.npy", "wide")
     assert np.array_equal(wide, base), "128 x 128 tiles (wide) differ from the default tiles"
