@@ -1033,7 +1033,8 @@ int ce_gpu_plan_destroy(ce_gpu_plan *p) {
 // CATEARS_SKIP (measurement builds only, -DCATEARS_DIAG: wrong results, timing
 // only): launches left out of every call, to price each stage of a pipeline
 // by its absence -- 1 first GEMM layer, 2 finalize, 4 fbank, 8 CMVN, 16 last
-// GEMM layer, 32 the hidden GEMM layers.  0 in the product library.
+// GEMM layer, 32 the hidden GEMM layers, 64 the int8 path's min / max and
+// Quantize passes.  0 in the product library.
 static int diag_skip() {
 #ifdef CATEARS_DIAG
   static const int v = [] {
@@ -1506,12 +1507,14 @@ static int run_steps_i8(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x, 
         const int zero[1] = {0};
         const int nseg = L.spliced ? st.gemm.nseg : 1;
         const int *offs = L.spliced ? st.gemm.off : zero;
-        if (fused_parts > 0)
-          CE_TRY(launch_i8_params_fold(ctx->stream, part, fused_parts, params));
-        else
-          CE_TRY(launch_i8_params(ctx->stream, x, ldx, rows, L.in_width, rm, row_edge, L.in_left, L.in_right,
-                                  part, params));
-        CE_TRY(launch_i8_quantize(ctx->stream, x, ldx, rows, L.in_width, rm, nseg, offs, params, xq, ldq, rowsum));
+        if (!(diag_skip() & 64)) {  // measurement library: 64 leaves the int8 quantize passes out
+          if (fused_parts > 0)
+            CE_TRY(launch_i8_params_fold(ctx->stream, part, fused_parts, params));
+          else
+            CE_TRY(launch_i8_params(ctx->stream, x, ldx, rows, L.in_width, rm, row_edge, L.in_left, L.in_right,
+                                    part, params));
+          CE_TRY(launch_i8_quantize(ctx->stream, x, ldx, rows, L.in_width, rm, nseg, offs, params, xq, ldq, rowsum));
+        }
       }
       // the next step reads this GEMM's output directly: its min / max is
       // reduced in this GEMM's epilogue (the partials are read by the next
