@@ -299,24 +299,23 @@ def sink_share_default(world):
     return max(0.5, min(1.0, 1.066 - 0.055 * (world - 1)))
 
 
-CLOCK_GHZ = 2.4  # MI355X peak engine clock (MI355X_MICROARCH.md)
-
-
 def pmc_valu(kernel):
-    """SQ_INSTS_VALU of `kernel` per C2 launch from the newest committed
-    exact-fbank PMC summary (tools/pmc_kernel.sh over `--workload c2`, the
-    998 000-frame launch); None if there is none or the kernel is not in it."""
+    """Measured VALU occupancy of `kernel` in the C2 launch from the newest
+    committed counter summary (tools/pmc_valu.py over one rocprofv3 --pmc
+    pass of `bench.py --workload c2`, tools/round_gpu.sh); None if there is
+    none or the kernel is not in it."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_c2_pmc_fbank*.txt")), reverse=True)
     base = kernel.split("<")[0]
     tmpl = kernel.split("<")[1].rstrip("*") if "<" in kernel else ""
-    for f in files:  # the newest summary that has this kernel
-        name = None
-        for ln in open(f):
-            if ln.startswith("void "):
-                name = ln.strip()[5:]
-            elif "SQ_INSTS_VALU" in ln and name and kernel_match(name, base + "*") and tmpl.split("*")[0] in name:
-                return {"instructions": float(ln.split()[-1]), "frames": 998000, "source": os.path.relpath(f, ROOT)}
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_c2_pmc_valu.json")), reverse=True):
+        data = json.load(open(f))
+        for name, v in data.get("kernels", {}).items():
+            if kernel_match(name, base + "*") and tmpl.split("*")[0] in name:
+                return dict(v, source=os.path.relpath(f, ROOT),
+                            definition="tools/pmc_valu.py: valu_active_per_simd = SQ_ACTIVE_INST_VALU / "
+                                       "(4 SQ_BUSY_CU_CYCLES); valu_busy_amd = AMD's VALUBusy; valu_issue_2cyc = "
+                                       "SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x cycles); wave_* = fractions "
+                                       "of SQ_WAVE_CYCLES")
     return None
 
 
@@ -525,12 +524,14 @@ def main_c2(args):
         ctx.profile(True)
     if world > 1:
         dist.barrier()
+    gpu.trace_mark(local, stream, 1)  # the timed window, for tools/trace_summary.py --window
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         gpu.fbank(ctx, plan, pcm, feats)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    gpu.trace_mark(local, stream, 2)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -558,17 +559,11 @@ def main_c2(args):
                     "kernel": kname, "launches": len(iv), "avg_launch_ms": round(avg_ms, 4),
                     "algorithmic_bytes_per_launch": bytes_per_launch,
                     "valu_flops_per_frame": 14000}
-        # the bound the kernel actually meets: VALU issue (PMC instruction
-        # count of the committed kernel x 4 cycles per wave64 instruction on
-        # a 16-lane SIMD, over the 1024 SIMDs, against this launch's time)
+        # what the kernel's SIMDs did, from the committed PMC pass of this
+        # workload (the HBM figure above is the contract's named bound)
         valu = pmc_valu(kname)
         if valu is not None:
-            n_launch = valu["frames"]
-            instr = valu["instructions"] * plan.total_frames / n_launch
-            need_ms = instr * 4 / 1024 / (CLOCK_GHZ * 1e6)
-            roofline["valu_issue"] = {"instructions_per_launch": round(instr), "ms_at_issue_rate": round(need_ms, 4),
-                                      "frac": round(need_ms / avg_ms, 3), "clock_ghz": CLOCK_GHZ,
-                                      "source": valu["source"]}
+            roofline["valu_counters"] = valu
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         threads, how = usable_cores()
@@ -761,6 +756,7 @@ def main_c4(args):
             c.profile(True, classes=None if args.stage_profile else [ctxs[0].PROF_GEMM])
     if world > 1:
         dist.barrier()
+    gpu.trace_mark(local, backs[0], 1)  # the timed window, for tools/trace_summary.py --window
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     if batches:
@@ -777,6 +773,7 @@ def main_c4(args):
             gat.drain()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    gpu.trace_mark(local, backs[0], 2)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -901,10 +898,10 @@ def verify_serial(args, kept, ctx, model, plan, pcm, gstats, U, pool):
         d_sum = psums.view(torch.int64) != sums.view(torch.int64)
         if bool(d_raw.any()) or bool(d_norm.any()) or bool(d_sum.any()):
             rows = torch.nonzero(d_raw.any(1)).flatten().tolist()
-            # where each differing frame ran: fast mode = 16 lanes per frame,
-            # 4 frames per wave, 4 waves per block; exact = 8 lanes, 8 frames
-            # per wave, 8 waves per block (one grid pass at C3)
-            lanes, fpw, wpb = (16, 4, 4) if args.fbank == "fast" else (8, 8, 8)
+            # where each differing frame ran: both modes build fbank.hip's
+            # lane program -- 8 lanes per frame, 8 frames per wave, 8 waves
+            # per block (one grid pass at C3)
+            lanes, fpw, wpb = 8, 8, 8
             where = []
             for r in rows[:4]:
                 bands = torch.nonzero(d_raw[r]).flatten().tolist()
@@ -1043,8 +1040,14 @@ def main(argv=None):
         hio = {"up": torch.cuda.Stream(), "down": torch.cuda.Stream(),
                "down_done": [None] * nbuf}
 
+    # front slots (raw / norm / PCM buffers) go by the scored ordinal, not the
+    # step: with a sink share below 1 the scored steps are not consecutive,
+    # and front_stage(todo[k + 1]) runs before back_stage(todo[k]), so two
+    # scored steps must never share a slot
+    slot_of, n_scored = {}, [0]
+
     def front_stage(i):
-        slot = i % F
+        slot = slot_of[i]
         front, ctx_f = fronts[i % NF], ctx_fs[i % NF]
         front.wait_event(free[slot])  # the batch F steps ago has finished reading this slot
         first = (i * U) % (pool - U + 1)
@@ -1065,7 +1068,7 @@ def main(argv=None):
         ready[slot].record(front)
 
     def back_stage(i):
-        slot, o, b = i % F, i % nbuf, i % NB
+        slot, o, b = slot_of[i], i % nbuf, i % NB
         stream = backs[b]
         if gat is not None:
             # the gather from nbuf steps ago has read outs[o]: only this
@@ -1156,6 +1159,9 @@ def main(argv=None):
 
     def run(first, count):
         todo = [i for i in range(first, first + count) if scores(i)]
+        for i in todo:
+            slot_of[i] = n_scored[0] % F
+            n_scored[0] += 1
         wide = set()
         if todo and args.wide_tiles != "none":
             wide = {todo[-1]} | ({todo[0]} if args.wide_tiles == "ends" else set())
@@ -1203,6 +1209,7 @@ def main(argv=None):
             c.profile(True, classes=None if args.stage_profile or int8 else [ctx.PROF_GEMM])
     if world > 1:
         dist.barrier()
+    gpu.trace_mark(local, backs[0], 1)  # the timed window, for tools/trace_summary.py --window
     torch.cuda.synchronize()
     step_ev = [] if args.step_times else None
     if step_ev is not None:
@@ -1214,6 +1221,7 @@ def main(argv=None):
         gat.drain()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    gpu.trace_mark(local, backs[0], 2)
     if step_ev is not None:
         print(json.dumps({"rank": rank, "wall_ms": round(elapsed * 1e3, 4),
                           "step_done_ms": [round(win.elapsed_time(e), 4) for e in step_ev]}), file=sys.stderr)

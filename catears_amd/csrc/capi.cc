@@ -391,18 +391,20 @@ static int upload_f16(const std::vector<float> &wt, int n, int kpad, DevBuf *out
   return out->upload(sp.data(), sp.size() * 2);
 }
 
-// Default matrix-core form of the fp32 program (CATEARS_NNET_GEMM overrides).
+#ifdef CATEARS_DIAG
+int knob_env(const char *name, int dflt) {
+  const char *e = getenv(name);
+  return e && *e ? atoi(e) : dflt;
+}
+#endif
+
+// Default matrix-core form of the fp32 program: bf16x6.  Another mode is a
+// per-model choice through ce_gpu_model_set_gemm; the experiments library
+// also takes CATEARS_NNET_GEMM (0 fp32, 1 bf16x6, 2 f16x3, 3 bf16x6p, the
+// ce_gpu_model_set_gemm numbers) for the tools.
 static int default_gemm() {
-  static const int g = [] {
-    const char *e = getenv("CATEARS_NNET_GEMM");
-    if (e && !strcmp(e, "fp32")) return (int)CE_GPU_GEMM_FP32;
-    if (e && !strcmp(e, "bf16x6")) return (int)CE_GPU_GEMM_BF16X6;
-    if (e && !strcmp(e, "f16x3")) return (int)CE_GPU_GEMM_F16X3;
-    if (e && !strcmp(e, "bf16x6p")) return (int)CE_GPU_GEMM_BF16X6_PLANES;
-    if (e && *e) return -1;  // unknown mode: model loads fail (CE_GPU_EINVAL)
-    return (int)CE_GPU_GEMM_BF16X6;
-  }();
-  return g;
+  static const int g = CE_KNOB("CATEARS_NNET_GEMM", (int)CE_GPU_GEMM_BF16X6);
+  return g >= CE_GPU_GEMM_FP32 && g <= CE_GPU_GEMM_BF16X6_PLANES ? g : -1;
 }
 
 static int build_program(const std::vector<RawLayer> &layers, int left, int right, ce_gpu_model *m) {
@@ -543,9 +545,7 @@ static int build_program(const std::vector<RawLayer> &layers, int left, int righ
   }
   m->x3_ok = m->x3_ok && m->x6_ok;
   const int want = default_gemm();
-  if (want < 0)
-    return fail(CE_GPU_EINVAL, std::string("CATEARS_NNET_GEMM=") + getenv("CATEARS_NNET_GEMM") +
-                                   ": not one of fp32, bf16x6, bf16x6p, f16x3");
+  if (want < 0) return fail(CE_GPU_EINVAL, "default GEMM mode: not one of 0 fp32, 1 bf16x6, 2 f16x3, 3 bf16x6p");
   m->gemm = want == CE_GPU_GEMM_F16X3 && m->x3_ok   ? CE_GPU_GEMM_F16X3
             : want == CE_GPU_GEMM_BF16X6_PLANES && m->x6_ok ? CE_GPU_GEMM_BF16X6_PLANES
             : want != CE_GPU_GEMM_FP32 && m->x6_ok ? CE_GPU_GEMM_BF16X6
@@ -810,6 +810,12 @@ int ce_gpu_profile_anchor(int device, void *stream) {
   return CE_GPU_OK;
 }
 
+int ce_gpu_trace_mark(int device, void *stream, int tag) {
+  if (device < 0 || device >= 64 || tag < 1 || tag > 64) return fail(CE_GPU_EINVAL, "bad device or tag");
+  CE_HIP(hipSetDevice(device));
+  return launch_trace_mark(static_cast<hipStream_t>(stream), tag);
+}
+
 int ce_gpu_ctx_profile_intervals(ce_gpu_ctx *ctx, int kernel_class, double *h_start_ms, double *h_end_ms,
                                  int capacity, int *count) {
   if (!ctx || !count || kernel_class < 0 || kernel_class >= CE_GPU_PROF_CLASSES)
@@ -1036,15 +1042,8 @@ int ce_gpu_plan_destroy(ce_gpu_plan *p) {
 // GEMM layer, 32 the hidden GEMM layers, 64 the int8 path's min / max and
 // Quantize passes.  0 in the product library.
 static int diag_skip() {
-#ifdef CATEARS_DIAG
-  static const int v = [] {
-    const char *e = getenv("CATEARS_SKIP");
-    return e ? atoi(e) : 0;
-  }();
+  static const int v = CE_KNOB("CATEARS_SKIP", 0);
   return v;
-#else
-  return 0;
-#endif
 }
 
 extern "C" {
@@ -1081,12 +1080,10 @@ int ce_gpu_cmvn(ce_gpu_ctx *ctx, const ce_gpu_plan *p, const float *d_global_sta
 }  // extern "C"
 
 namespace catears {
-// CATEARS_SPLICE_FIRST=0 keeps the gather loader for narrow segments (A/B).
+// CATEARS_SPLICE_FIRST=0 (experiments library) keeps the gather loader for
+// narrow segments (A/B).
 static bool splice_first_layer() {
-  static const bool on = [] {
-    const char *e = getenv("CATEARS_SPLICE_FIRST");
-    return !e || atoi(e) != 0;
-  }();
+  static const bool on = CE_KNOB("CATEARS_SPLICE_FIRST", 1) != 0;
   return on;
 }
 
@@ -1165,28 +1162,19 @@ static int run_steps_f32(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
 // Default; CATEARS_X6_F32IN=0 selects the plane-operand kernels
 // (run_steps_x6: planes written by each epilogue, bit-identical results).
 static int x6_variant_env() {
-  static const int v = [] {
-    const char *e = getenv("CATEARS_X6_VARIANT");
-    return e ? atoi(e) : 0;
-  }();
+  static const int v = CE_KNOB("CATEARS_X6_VARIANT", 0);
   return v;
 }
 
 static bool x6_f32in() {
-  static const bool v = [] {
-    const char *e = getenv("CATEARS_X6_F32IN");
-    return !e || atoi(e) != 0;
-  }();
+  static const bool v = CE_KNOB("CATEARS_X6_F32IN", 1) != 0;
   return v;
 }
 
 // CATEARS_X6_FIRST=0 keeps the round-3 splice_pad launch before the first
 // layer's throughput GEMM (bit-identical; the default gathers in its loader)
 static bool x6_first_direct() {
-  static const bool v = [] {
-    const char *e = getenv("CATEARS_X6_FIRST");
-    return !e || atoi(e) != 0;
-  }();
+  static const bool v = CE_KNOB("CATEARS_X6_FIRST", 1) != 0;
   return v && (x6_variant_env() == 0 || x6_variant_env() == 300);
 }
 
@@ -1198,20 +1186,14 @@ static bool x6_first_direct() {
 // 2: only the output layer reads planes (its 14 unit tiles would each split
 // the same activations), written by the layer before it.
 static int x6_plane_chain_env() {
-  static const int v = [] {
-    const char *e = getenv("CATEARS_X6_CHAIN");
-    return e ? atoi(e) : 0;
-  }();
+  static const int v = CE_KNOB("CATEARS_X6_CHAIN", 0);
   return v;
 }
 
 // CATEARS_LAT_FUSED_FINAL=0 keeps the last layer's split-K reduce as its own
 // launch before the finalize (bit-identical; the default fuses the two)
 static bool lat_fused_final() {
-  static const bool v = [] {
-    const char *e = getenv("CATEARS_LAT_FUSED_FINAL");
-    return !e || atoi(e) != 0;
-  }();
+  static const bool v = CE_KNOB("CATEARS_LAT_FUSED_FINAL", 1) != 0;
   return v;
 }
 

@@ -31,6 +31,22 @@ int hip_fail(hipError_t e, const char *what);
     if (rc_ != CE_GPU_OK) return rc_; \
   } while (0)
 
+// -------------------------------------------------- measurement knobs --
+
+// CE_KNOB("CATEARS_...", default): a tuning switch of the measurement tools
+// (tools/).  Only the experiments library (make EXPERIMENTS=1,
+// -DCATEARS_DIAG) reads it from the environment; the product library
+// compiles the default in, so its behaviour never depends on the
+// environment and no CATEARS_* name is in it (tests/test_abi.py).  Model and
+// context choices go through the C-ABI (ce_gpu_model_set_gemm,
+// ce_gpu_ctx_set_latency / _set_fbank / _set_wide_tiles).
+#ifdef CATEARS_DIAG
+int knob_env(const char *name, int dflt);  // getenv + atoi, read once per name by the caller
+#define CE_KNOB(name, dflt) ::catears::knob_env(name, dflt)
+#else
+#define CE_KNOB(name, dflt) (dflt)
+#endif
+
 // ------------------------------------------------------- device buffers --
 
 // Owning device allocation (hipMalloc); never copied.
@@ -503,6 +519,7 @@ constexpr int kPropagateWindow = 1 << 16;
 int launch_finalize(hipStream_t s, const float *x, int ldx, int rows, int dim, bool log_softmax,
                     const float *log_prior, const int *row_dst, float *out);
 int launch_rowop(hipStream_t s, const RowOp &op, float *x, int ldx, int rows);
+int launch_trace_mark(hipStream_t s, int tag);
 int launch_loglik_gather(hipStream_t s, const float *ll, int rows, int ld, int dim, const int32_t *tpm, int n_tid,
                          const int32_t *row, const int32_t *trans, int n, float scale, float *out);
 int launch_loglik_columns(hipStream_t s, const float *ll, int rows, int ld, int dim, const int32_t *cols,

@@ -1251,10 +1251,7 @@ int launch_r(hipStream_t s, X6Args p) {
 // vs 155.6 us, C3 at the driver's flags 6.36-6.38 vs 6.40-6.46 M frames/s --
 // so one stays the default; the barrier is not what the loop waits on.
 int x6_ks() {
-  static int v = [] {
-    const char *e = getenv("CATEARS_X6_KS");
-    return e ? atoi(e) : 1;
-  }();
+  static int v = CE_KNOB("CATEARS_X6_KS", 1);
   return v;
 }
 
@@ -1294,21 +1291,18 @@ int launch_ws(hipStream_t s, X6Args p) {
   return CE_GPU_OK;
 }
 
-// CATEARS_X6_VARIANT: the schedule of the fp32-activation bf16x6 GEMM.
-// The product build carries the default (0 = 300, direct weights: 256 x 128
-// tiles, weight fragments straight from L2 to registers), the round-2
+// CATEARS_X6_VARIANT (experiments library only, CE_KNOB): the schedule of
+// the fp32-activation bf16x6 GEMM.  The product build runs the default (0 =
+// 300, direct weights: 256 x 128 tiles, weight fragments straight from L2 to
+// registers) and, for a model without the fragment image, the round-2
 // default 160 (region-scheduled 128 x 256 tiles, weights split in the
-// kernel) and the two documented deployment alternatives, all bit-identical
-// (tests/test_gpu_x6_variants.py): 40 (128 x 128 tiles, one batch at a time
-// on an idle GPU) and 200 (warp-specialised 128 x 128).  Measurement
-// variants -- and the DIAG ablations, which give wrong results -- exist only
-// in `make EXPERIMENTS=1` builds (libcatears_hip_exp.so, tools/); any other
-// value makes every bf16x6 launch fail with CE_GPU_EINVAL.
+// kernel).  The bit-identical alternatives -- 40 (128 x 128 tiles), 200
+// (warp-specialised 128 x 128), the measurement variants -- and the DIAG
+// ablations, which give wrong results, exist only in `make EXPERIMENTS=1`
+// builds (libcatears_hip_exp.so, tools/, tests/test_gpu_x6_variants.py);
+// any other value there makes every bf16x6 launch fail with CE_GPU_EINVAL.
 int x6_variant() {
-  static int v = [] {
-    const char *e = getenv("CATEARS_X6_VARIANT");
-    return e ? atoi(e) : 0;
-  }();
+  static int v = CE_KNOB("CATEARS_X6_VARIANT", 0);
   return v;
 }
 
@@ -1317,10 +1311,7 @@ int x6_variant() {
 // 20.9 us per launch in a serial run (r4c); 256: the hidden layers' tiles.
 // Same bits either way (tests/test_gpu_x6_variants.py).
 int x6_first_tile() {
-  static int v = [] {
-    const char *e = getenv("CATEARS_X6_FIRST_TILE");
-    return e ? atoi(e) : 128;
-  }();
+  static int v = CE_KNOB("CATEARS_X6_FIRST_TILE", 128);
   return v;
 }
 
@@ -1430,13 +1421,13 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
           return launch_d<X6Cfg<kX6DirUnits, 128, 4, 2, 2>>(s, p);
         }
         [[fallthrough]];
-      case 160:  // region-scheduled fp32-operand loop (round-2 default)
+      case 160:  // region-scheduled fp32-operand loop (round-2 default; a model without the fragment image)
         return launch_f<X6Cfg<128, 256, 2, 4, 2>, 8>(s, p);
+#ifdef CATEARS_EXPERIMENTS
       case 40:  // 128 x 128 tiles: fills all CUs on a 1024-wide layer (one batch at a time on an idle GPU)
         return launch_f<X6Cfg<128, 128, 4, 2, 2>>(s, p);
       case 200:  // warp-specialised: 4 MFMA waves (64 x 64 each) + 4 producer waves
         return launch_ws<X6Cfg<128, 128, 2, 2, 2>, 4>(s, p);
-#ifdef CATEARS_EXPERIMENTS
       // 400: register-direct, both operands straight to registers, no LDS
       // (bit-identical; C3 4.50-4.52 vs 5.67-5.69 M frames/s, serial layers
       // 0.183 vs 0.127 ms: the activation fragments fetched by all four waves
@@ -1527,9 +1518,8 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
         return launch_f<X6Cfg<128, 256, 2, 4, 2>, 6, 43>(s, p);
 #endif
       default:
-        return fail(CE_GPU_EINVAL, "CATEARS_X6_VARIANT=" + std::to_string(x6_variant()) +
-                                       " is not a schedule of this build (product: 0, 300, 160, 40, 200; others need "
-                                       "`make EXPERIMENTS=1`)");
+        return fail(CE_GPU_EINVAL, "bf16x6 schedule " + std::to_string(x6_variant()) +
+                                       " is not in this build (the experiments library: `make EXPERIMENTS=1`)");
     }
   }
   // plane operands (CATEARS_X6_F32IN=0 / CE_GPU_GEMM_BF16X6_PLANES)

@@ -331,10 +331,7 @@ __global__ __launch_bounds__(64) void lat_reduce_kernel(LatReduceArgs p) {
 // re-read per tile.  The partition changes which block computes a tile, never
 // the tile's sums.
 int lat_rtb(int row_tiles, int blocks_per_tile) {
-  static const int env = [] {
-    const char *e = getenv("CATEARS_LAT_RTB");
-    return e ? atoi(e) : 0;
-  }();
+  static const int env = CE_KNOB("CATEARS_LAT_RTB", 0);
   const int rtb = env > 0 ? env : row_tiles * blocks_per_tile / (2 * kLatTarget);
   return std::max(1, std::min(rtb, row_tiles));
 }
@@ -342,10 +339,7 @@ int lat_rtb(int row_tiles, int blocks_per_tile) {
 template <int TF, int KT>
 void launch_lat_gemm_kt(hipStream_t s, const LatArgs &p, dim3 grid, dim3 block) {
 #ifdef CATEARS_DIAG
-  static const int diag = [] {
-    const char *e = getenv("CATEARS_LAT_DIAG");
-    return e ? atoi(e) : 0;
-  }();
+  static const int diag = CE_KNOB("CATEARS_LAT_DIAG", 0);
   switch (diag) {
     case 0: break;
 #define CE_LAT_DIAG(D) \
@@ -384,16 +378,8 @@ void launch_lat_gemm(hipStream_t s, LatArgs p) {
 // the blocks per row tile the slice rule aims at (default kLatTarget); other
 // values change the fp32 summation order, so the product library ignores it.
 static int lat_target() {
-#ifdef CATEARS_EXPERIMENTS
-  static const int v = [] {
-    const char *e = getenv("CATEARS_LAT_TARGET");
-    const int t = e ? atoi(e) : 0;
-    return t > 0 ? t : kLatTarget;
-  }();
-  return v;
-#else
-  return kLatTarget;
-#endif
+  static const int v = CE_KNOB("CATEARS_LAT_TARGET", 0);
+  return v > 0 ? v : kLatTarget;
 }
 
 int x6_lat_slices(int kpad, int n) {

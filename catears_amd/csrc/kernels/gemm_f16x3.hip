@@ -299,10 +299,7 @@ int launch_cfg(hipStream_t s, X3Args p, bool out16) {
 }
 
 int x3_variant() {
-  static int v = [] {
-    const char *e = getenv("CATEARS_X3_VARIANT");
-    return e ? atoi(e) : 0;
-  }();
+  static int v = CE_KNOB("CATEARS_X3_VARIANT", 0);
   return v;
 }
 
@@ -375,8 +372,8 @@ int launch_gemm_f16x3(hipStream_t s, const X3Gemm &a) {
                  : launch_cfg<X3Cfg<128, 256, 2, 4, 3, 32>>(s, p, out16);
 #endif
     default:
-      return fail(CE_GPU_EINVAL, "CATEARS_X3_VARIANT=" + std::to_string(x3_variant()) +
-                                     " is not a kernel of this build (product: 0; others need `make EXPERIMENTS=1`)");
+      return fail(CE_GPU_EINVAL, "f16x3 variant " + std::to_string(x3_variant()) +
+                                     " is not in this build (the experiments library: `make EXPERIMENTS=1`)");
   }
 }
 

@@ -702,10 +702,7 @@ int launch_glds(hipStream_t s, KArgs p, bool a_fast, bool b_nmajor, bool rm) {
 constexpr int kDefaultVariant = 29;
 
 int variant() {
-  static int v = [] {
-    const char *e = getenv("CATEARS_GEMM_VARIANT");
-    return e ? atoi(e) : kDefaultVariant;
-  }();
+  static int v = CE_KNOB("CATEARS_GEMM_VARIANT", kDefaultVariant);
   return v;
 }
 
@@ -744,10 +741,7 @@ int launch_gemm_f32(hipStream_t s, const GemmArgs &a) {
   for (int i = 0; i < 4; ++i) p.post[i] = a.post[i];
   p.npost = a.npost;
   p.post_mode = post_mode(a.post, a.npost);
-  static const int group_env = [] {
-    const char *e = getenv("CATEARS_GEMM_GROUP");
-    return e ? atoi(e) : 0;
-  }();
+  static const int group_env = CE_KNOB("CATEARS_GEMM_GROUP", 0);
   p.group = group_env > 0 ? group_env : 16;  // tools: group sweep (16 >= 8 > 4 by 0.3-0.6 %)
   // fast A path: every K-tile inside one segment, float4-aligned rows
   const bool a_fast = (a.ldx % 4 == 0) && ((reinterpret_cast<uintptr_t>(a.x) & 15) == 0);
@@ -834,8 +828,8 @@ int launch_gemm_f32(hipStream_t s, const GemmArgs &a) {
       return deep ? launch_glds<V1, 2>(s, p, a_fast, a.b_nmajor, rm) : launch_glds<V0, 2>(s, p, a_fast, a.b_nmajor, rm);
 #endif
     default:
-      return fail(CE_GPU_EINVAL, "CATEARS_GEMM_VARIANT=" + std::to_string(variant()) +
-                                     " is not a kernel of this build (product: 29; others need `make EXPERIMENTS=1`)");
+      return fail(CE_GPU_EINVAL, "gemm_f32 variant " + std::to_string(variant()) +
+                                     " is not in this build (the experiments library: `make EXPERIMENTS=1`)");
   }
 }
 

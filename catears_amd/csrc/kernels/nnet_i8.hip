@@ -1127,16 +1127,11 @@ int launch_i8_gemm(hipStream_t s, const I8Layer &L, const int8_t *a, int lda, in
   p.post_mode = post_mode(L.post, L.npost);
   p.y = y;
   p.ldy = ldy;
-  static const int vec_epi = [] {
-    const char *e = getenv("CATEARS_I8_EPI");
-    return e ? atoi(e) : 1;
-  }();
+  static const int vec_epi = CE_KNOB("CATEARS_I8_EPI", 1);
   p.vec_epi = vec_epi && L.n % 4 == 0 && ldy % 4 == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0;
 
-  static const int use_glds = [] {
-    const char *e = getenv("CATEARS_I8_GEMM");
-    return e ? atoi(e) : 16;  // measured best on TDNN-S, frame batch 8192 (tools/i8_sweep.sh)
-  }();
+  // 16: measured best on TDNN-S, frame batch 8192 (tools/i8_sweep.sh)
+  static const int use_glds = CE_KNOB("CATEARS_I8_GEMM", 16);
   if (use_glds && p.kpad % 128 == 0 && p.din % 128 == 0 && lda % 16 == 0) {
     auto go = [&](auto kern, int bm, int bn, int threads = 256) {
       p.tiles_n = (L.n + bn - 1) / bn;
@@ -1201,9 +1196,8 @@ int launch_i8_gemm(hipStream_t s, const I8Layer &L, const int8_t *a, int lda, in
       case 1: go(gemm_i8_glds_kernel<128, 128, 2>, 128, 128); break;
 #endif
       default:
-        return fail(CE_GPU_EINVAL, "CATEARS_I8_GEMM=" + std::to_string(use_glds) +
-                                       " is not a kernel of this build (product: 16, 15, or 0 for the register-staged "
-                                       "fallback; others need `make EXPERIMENTS=1`)");
+        return fail(CE_GPU_EINVAL, "int8 GEMM variant " + std::to_string(use_glds) +
+                                       " is not in this build (the experiments library: `make EXPERIMENTS=1`)");
     }
     CE_HIP(hipGetLastError());
     return CE_GPU_OK;

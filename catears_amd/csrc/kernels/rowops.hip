@@ -321,9 +321,11 @@ namespace {
 // buffer in double -- four accumulators, one per load slot, so four loads are
 // in flight per thread -- then a fixed wave / block tree, one partial per
 // block, and one wave folds the partials in block order.  The order depends
-// on the buffer sizes only: the same bytes give the same double.  Several
-// buffers share one launch pair (rank 0 folds every peer's rows of a step
-// at once).
+// on the buffer sizes, on each buffer's 16-byte alignment (float4 or scalar
+// path) and on the list of buffers folded together (shared accumulators, a
+// grid sized by the largest): the same buffers at the same alignments give
+// the same double (include/catears_gpu.h).  Several buffers share one launch
+// pair (rank 0 folds every peer's rows of a step at once).
 constexpr int kSumThreads = 256;
 constexpr int kSumMaxBufs = 16;
 
@@ -403,6 +405,18 @@ int launch_sum_f64(hipStream_t s, int count, const float *const *x, const int64_
 
 int launch_rowop(hipStream_t s, const RowOp &op, float *x, int ldx, int rows) {
   return launch_rowop_raw(s, op.kind, op.dim, op.scale.as<float>(), op.offset.as<float>(), x, ldx, rows);
+}
+
+namespace {
+// ce_gpu_trace_mark: a kernel that does nothing, seen by a kernel trace under
+// its name with `tag` workgroups (the window markers of bench.py's timed steps)
+__global__ __launch_bounds__(64) void trace_mark_kernel() {}
+}  // namespace
+
+int launch_trace_mark(hipStream_t s, int tag) {
+  hipLaunchKernelGGL(trace_mark_kernel, dim3(tag), dim3(64), 0, s);
+  CE_HIP(hipGetLastError());
+  return CE_GPU_OK;
 }
 
 }  // namespace catears

@@ -32,7 +32,7 @@ ABI = [
     "ce_gpu_nnet_propagate_blocks", "ce_gpu_loglik_gather", "ce_gpu_loglik_columns",
     "ce_gpu_model_set_gemm", "ce_gpu_model_get_gemm", "ce_gpu_ctx_overflow", "ce_gpu_ctx_set_latency",
     "ce_gpu_fbank_s16", "ce_gpu_score_s16", "ce_gpu_ctx_set_fbank", "ce_gpu_sum_f64", "ce_gpu_ctx_set_wide_tiles",
-    "ce_gpu_sum_f64_many",
+    "ce_gpu_sum_f64_many", "ce_gpu_trace_mark",
 ]
 
 # ce_gpu_model_set_gemm modes
@@ -89,6 +89,7 @@ def lib():
         "ce_gpu_gemm_u8u8f32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp]),
         "ce_gpu_gemm_u8u8i32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp]),
         "ce_gpu_profile_anchor": (ci, [ci, vp]),
+        "ce_gpu_trace_mark": (ci, [ci, vp, ci]),
         "ce_gpu_model_quantize": (ci, [vp, vp]),
         "ce_gpu_nnet_propagate_blocks": (ci, [vp, vp, vp, ci, ctypes.POINTER(ctypes.c_int32), ci, ci, vp]),
         "ce_gpu_ctx_profile_intervals": (ci, [vp, ci, vp, vp, ci, pi]),
@@ -285,6 +286,12 @@ class Model:
 def profile_anchor(device, stream):
     """Record the time origin for Context.profile_intervals on `stream`."""
     check(lib().ce_gpu_profile_anchor(device, ctypes.c_void_p(stream.cuda_stream)))
+
+
+def trace_mark(device, stream, tag):
+    """Launch the empty window-marker kernel with `tag` workgroups on `stream`
+    (tools/trace_summary.py --window cuts a rocprofv3 kernel trace at it)."""
+    check(lib().ce_gpu_trace_mark(device, ctypes.c_void_p(stream.cuda_stream), tag))
 
 
 def union_ms(intervals):

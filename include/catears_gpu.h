@@ -165,6 +165,14 @@ int ce_gpu_profile_anchor(int device, void *stream);
 int ce_gpu_ctx_profile_intervals(ce_gpu_ctx *ctx, int kernel_class, double *h_start_ms, double *h_end_ms,
                                  int capacity, int *count);
 
+/* Window marker for an external kernel trace (rocprofv3 --kernel-trace):
+ * launches one empty kernel, catears::trace_mark_kernel, of `tag` (1..64)
+ * workgroups on `stream`.  bench.py marks the start (tag 1) and end (tag 2)
+ * of its timed steps, and tools/trace_summary.py --window summarises only
+ * the launches between the two.  Measurement plumbing; no reference
+ * counterpart. */
+int ce_gpu_trace_mark(int device, void *stream, int tag);
+
 /* -------------------------------------------------------------- model --- */
 
 /* AcousticModel::Read (src/am.cc:26-64): reads the key=value config (keys
@@ -415,8 +423,13 @@ int ce_gpu_loglik_columns(ce_gpu_ctx *ctx, const float *d_loglik, int rows, int 
 /* *d_acc += the float64 sum of the n floats at d_x, on `stream` (a
  * hipStream_t; NULL = the null stream) of the current device; d_part is
  * device scratch for CE_GPU_SUM_PARTS doubles.  Each element is widened to
- * double before it is added, in an order that depends on n only (the same
- * bytes give the same sum).  No reference counterpart: the consumer of the
+ * double before it is added.  Deterministic, not order-free: the summation
+ * order depends on n, on whether d_x is 16-byte aligned (float4 or scalar
+ * loads) and, in the _many form, on the whole list of buffers (the grid is
+ * sized by the largest one and the buffers share per-thread accumulators) --
+ * the same buffers at the same alignments give the same bits, the same rows
+ * at another offset or folded with other buffers may differ in the last
+ * places.  No reference counterpart: the consumer of the
  * log-likelihood rows gathered to rank 0 -- bench.py and
  * catears_amd/shard.py RowGather fold every row into this checksum, at HBM
  * speed where torch's float64 reduction runs at about a third of it. */

@@ -8,6 +8,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 GOLDEN = os.path.join(ROOT, "tests", "golden", "ref")
+# the measurement build (make EXPERIMENTS=1): the same kernels plus the
+# tuning switches the product library compiles out (CE_KNOB, internal.h)
+EXP_LIB = os.path.join(ROOT, "catears_amd", "lib", "libcatears_hip_exp.so")
 
 
 def pytest_configure(config):
@@ -53,3 +56,12 @@ def global_stats():
     """test/data/cmvn_stats.bin payload (41 floats)."""
     from catears_amd import formats
     return formats.read_vec(os.path.join(GOLDEN, "cmvn_stats.bin"))
+
+
+@pytest.fixture(scope="session")
+def exp_lib():
+    """Path of the experiments library, for child processes that select an
+    alternative schedule through its CATEARS_* switches."""
+    if not os.path.exists(EXP_LIB):
+        pytest.skip("libcatears_hip_exp.so not built (make EXPERIMENTS=1 lib)")
+    return EXP_LIB

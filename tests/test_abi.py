@@ -68,6 +68,19 @@ def test_product_library_has_no_ablation_kernels():
     assert b"gemm_bf16x6r_kernel" not in data
 
 
+def test_product_library_reads_no_environment_switch():
+    """The tuning switches of the measurement tools (CE_KNOB, internal.h) are
+    read from the environment only by the experiments library; the product
+    library compiles their defaults in, so no CATEARS_* name
+    -- and no getenv call -- is in it.  Mode choices go through the C-ABI
+    (ce_gpu_model_set_gemm, ce_gpu_ctx_set_*).  The drop-in layer's
+    CATEARS_DEVICE / CATEARS_LANES / CATEARS_FBANK (host/src/runtime.cc,
+    libcatears_pk.so) are its documented configuration, not switches here."""
+    data = open(os.path.join(ROOT, "catears_amd", "lib", "libcatears_hip.so"), "rb").read()
+    assert re.findall(rb"CATEARS_[A-Z0-9_]+", data) == []
+    assert b"getenv" not in data
+
+
 def test_dropin_library_defines_no_test_hook():
     """The drop-in's failure injection is test-only: libcatears_pk.so holds an
     undefined weak reference to catears_test_inject_failure (null in every

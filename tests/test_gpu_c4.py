@@ -250,6 +250,18 @@ def test_c3_sink_share_rank0_scores_part_of_the_steps(tmp_path):
     assert two["checksum"] == pytest.approx(want, rel=1e-12)
 
 
+def test_c3_sink_share_serial_scores_the_right_steps(tmp_path):
+    """--serial with --sink-share 0.5 (two front slots; rank 0's scored steps
+    two apart): the next scored step's fbank + CMVN is staged before the
+    current one's nnet runs, so the front slots must go by the scored
+    ordinal, not the step -- every batch rank 0 scored matches a
+    serial re-score of the same step's utterances bit for bit."""
+    two = _bench_c3(["--serial", "--sink-share", "0.5", "--verify-serial"], 2)
+    assert two["config"]["rank0_scored_steps"] == 3
+    ver = two["verify_ranks"] if "verify_ranks" in two else [two["verify"]]
+    assert ver[0]["batches"] > 0 and all(v["differing"] == 0 for v in ver), ver
+
+
 def test_rehearse_peers_runs_and_reports():
     """bench.py --rehearse-peers (the one-GPU rehearsal of rank 0's receive +
     fold load behind the default sink share): it runs the

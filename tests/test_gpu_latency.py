@@ -135,14 +135,14 @@ np.save(sys.argv[2], np.concatenate(outs))
 """
 
 
-def test_latency_fused_final_reduce_exact(tmp_path, s_config):
+def test_latency_fused_final_reduce_exact(tmp_path, s_config, exp_lib):
     """The last layer's split-K reduce run inside the finalize (the default)
     gives the bits of its own reduce launch followed by the finalize
-    (CATEARS_LAT_FUSED_FINAL=0)."""
+    (CATEARS_LAT_FUSED_FINAL=0, a switch of the experiments library)."""
     from conftest import ROOT
     got = {}
     for flag in ("1", "0"):
-        env = dict(os.environ, CATEARS_LAT_FUSED_FINAL=flag, PYTHONPATH=ROOT)
+        env = dict(os.environ, CATEARS_LAT_FUSED_FINAL=flag, PYTHONPATH=ROOT, CATEARS_HIP_LIB=exp_lib)
         path = tmp_path / f"f{flag}.npy"
         r = subprocess.run([sys.executable, "-c", FUSED_CHILD, s_config, str(path)], env=env, capture_output=True,
                            text=True, timeout=300, cwd=ROOT)
@@ -232,14 +232,14 @@ def post_model_layers():
     return layers, left, right, prior
 
 
-def test_latency_fused_final_with_post_ops(tmp_path, oracle):
+def test_latency_fused_final_with_post_ops(tmp_path, oracle, exp_lib):
     """A last Linear followed by ReLU + BatchNorm: the fused finalize (the
     default) gives the bits of its own reduce launch and the finalize, and
-    the oracle's values."""
+    the oracle's values (experiments library, CATEARS_LAT_FUSED_FINAL)."""
     from conftest import ROOT
     got = {}
     for flag in ("1", "0"):
-        env = dict(os.environ, CATEARS_LAT_FUSED_FINAL=flag, PYTHONPATH=ROOT)
+        env = dict(os.environ, CATEARS_LAT_FUSED_FINAL=flag, PYTHONPATH=ROOT, CATEARS_HIP_LIB=exp_lib)
         path = tmp_path / f"p{flag}.npy"
         r = subprocess.run([sys.executable, "-c", POST_CHILD, str(path), os.path.join(ROOT, "tests")], env=env,
                            capture_output=True, text=True, timeout=300, cwd=ROOT)

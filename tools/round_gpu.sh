@@ -6,7 +6,7 @@ TAG=${TAG:-run}
 OUT="$R/gpurun_out/$TAG"
 mkdir -p "$OUT"
 cd "$R" || exit 1
-timeout -k 10 900 python -m pytest tests -q -m gpu -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1; rc=$?
+timeout -k 10 1200 python -u -m pytest tests -q -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -8 "$OUT/pytest_gpu.log"
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 [ -n "$SKIP_BENCH" ] && exit 0
@@ -46,6 +46,20 @@ for W in c2 c5; do
         > "$OUT/pmc_${W}_$i.log" 2>&1 || { echo "pmc $W $i failed"; tail -20 "$OUT/pmc_${W}_$i.log"; exit 1; }
   done
   python "$R/tools/pmc_traffic.py" "$OUT/pmc_${W}_1" "$OUT/pmc_${W}_2" "$OUT/pmc_traffic_$W.json"
+  if [ $W = c2 ]; then
+    # measured VALU occupancy of the fbank kernel (tools/pmc_valu.py): one pass, 7 SQ + 1 GRBM counters
+    timeout -k 10 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_BUSY_CU_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY \
+        SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-include-regex "fbank" \
+        --output-format csv -d "$OUT/pmc_${W}_3" -o run -- \
+        python "$R/bench.py" --workload $W --steps 3 --warmup 1 --no-cpu-baseline --no-profile --serial \
+        > "$OUT/pmc_${W}_3.log" 2>&1 || { echo "pmc $W 3 failed"; tail -20 "$OUT/pmc_${W}_3.log"; exit 1; }
+    timeout -k 10 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_BUSY_CU_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY \
+        SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-include-regex "fbank" \
+        --output-format csv -d "$OUT/pmc_${W}_4" -o run -- \
+        python "$R/bench.py" --workload $W --fbank fast --steps 3 --warmup 1 --no-cpu-baseline --no-profile --serial \
+        > "$OUT/pmc_${W}_4.log" 2>&1 || { echo "pmc $W 4 failed"; tail -20 "$OUT/pmc_${W}_4.log"; exit 1; }
+    python "$R/tools/pmc_valu.py" "$OUT/pmc_valu_$W.json" "$OUT/pmc_${W}_3" "$OUT/pmc_${W}_4"
+  fi
   if [ $W = c5 ]; then
     timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "gemm_" \
         --output-format csv -d "$OUT/pmc_${W}_3" -o run -- \
