@@ -36,10 +36,10 @@ HOSTFLAGS := -O2 -fPIC -std=c++17 -ffp-contract=off -Iinclude -I$(SRC) -I/opt/ro
              -D__HIP_PLATFORM_AMD__ -Wall $(EXPFLAGS)
 
 KERNELS := $(wildcard $(SRC)/kernels/*.hip)
-HOSTSRC := $(SRC)/capi.cc $(SRC)/tables.cc
+HOSTSRC := $(SRC)/capi.cc $(SRC)/tables.cc $(SRC)/model_io.cc
 OBJS := $(patsubst $(SRC)/kernels/%.hip,$(OBJ)/%.o,$(KERNELS)) \
         $(patsubst $(SRC)/%.cc,$(OBJ)/%.o,$(HOSTSRC))
-HDRS := include/catears_gpu.h $(SRC)/internal.h $(SRC)/fbank_ops.h $(SRC)/fbank8_ops.h $(SRC)/tile_order.h $(SRC)/lds_dma.h
+HDRS := include/catears_gpu.h $(SRC)/internal.h $(SRC)/model_io.h $(SRC)/fbank_ops.h $(SRC)/fbank8_ops.h $(SRC)/tile_order.h $(SRC)/lds_dma.h
 
 all: $(LIB) oracle
 

@@ -18,29 +18,14 @@
 #include <vector>
 
 #include "internal.h"
+#include "model_io.h"
 
 namespace catears {
 
 // ---------------------------------------------------------------- errors --
 
-static thread_local std::string g_last_error;
-
-int fail(int code, const std::string &msg) {
-  g_last_error = msg;
-  return code;
-}
-
 int hip_fail(hipError_t e, const char *what) {
   return fail(CE_GPU_EHIP, std::string(what) + ": " + hipGetErrorString(e));
-}
-
-static std::string fmt(const char *f, ...) {
-  char buf[1024];
-  va_list ap;
-  va_start(ap, f);
-  vsnprintf(buf, sizeof(buf), f, ap);
-  va_end(ap);
-  return buf;
 }
 
 // ---------------------------------------------------------------- DevBuf --
@@ -68,201 +53,6 @@ void DevBuf::release() {
   if (ptr) (void)hipFree(ptr);
   ptr = nullptr;
   bytes = 0;
-}
-
-// ----------------------------------------------------------- file reading --
-
-// Little-endian binary reader with the reference's error strings
-// (src/util.cc:123-153).
-struct Reader {
-  FILE *f = nullptr;
-  std::string name;
-  ~Reader() {
-    if (f) fclose(f);
-  }
-  int open(const std::string &path) {
-    name = path;
-    f = fopen(path.c_str(), "rb");
-    if (!f) return fail(CE_GPU_EIO, "IOError: Unable to open " + path);
-    return CE_GPU_OK;
-  }
-  // The same over an in-memory image (ce_gpu_model_load_mem).
-  int open_mem(const void *buf, size_t n, const char *label) {
-    name = label;
-    f = n ? fmemopen(const_cast<void *>(buf), n, "rb") : nullptr;
-    if (!f) return fail(CE_GPU_EIO, std::string("IOError: Unable to open ") + label);
-    return CE_GPU_OK;
-  }
-  int read(void *dst, size_t n) {
-    if (n == 0) return CE_GPU_OK;
-    if (fread(dst, n, 1, f) != 1) return fail(CE_GPU_EIO, "IOError: failed to read: " + name);
-    return CE_GPU_OK;
-  }
-  int i32(int32_t *v) { return read(v, 4); }
-  int tag(const char *expect) {
-    char got[5] = {0};
-    CE_TRY(read(got, 4));
-    if (memcmp(got, expect, 4) != 0)
-      return fail(CE_GPU_ECORRUPT, fmt("Corruption: ReadAndVerifyString: '%s' expected but '%s' found in %s",
-                                       expect, got, name.c_str()));
-    return CE_GPU_OK;
-  }
-  // Vector<Real>::Read (src/vector.cc:267-300), Real of size 4
-  template <typename T>
-  int vec(std::vector<T> *out) {
-    static_assert(sizeof(T) == 4, "VEC0 payloads here are 4-byte");
-    CE_TRY(tag("VEC0"));
-    int32_t section = 0, dim = 0;
-    CE_TRY(i32(&section));
-    CE_TRY(i32(&dim));
-    if (dim < 0 || (int64_t)dim * 4 + 4 != section)
-      return fail(CE_GPU_ECORRUPT, fmt("Corruption: section_size = %d * 4 + 4 expected, but %d found: %s",
-                                       dim, section, name.c_str()));
-    out->resize(dim);
-    return read(out->data(), (size_t)dim * 4);
-  }
-  // Matrix<float>::Read (src/matrix.cc:159-191)
-  int mat(std::vector<float> *out, int *rows, int *cols) {
-    CE_TRY(tag("MAT0"));
-    int32_t section = 0, r = 0, c = 0;
-    CE_TRY(i32(&section));
-    CE_TRY(i32(&r));
-    CE_TRY(i32(&c));
-    if (r < 0 || c < 0) return fail(CE_GPU_ECORRUPT, "Corruption: negative matrix shape in " + name);
-    out->resize((size_t)r * c);
-    std::vector<float> row;
-    for (int i = 0; i < r; ++i) {
-      CE_TRY(vec(&row));
-      if ((int)row.size() != c)
-        return fail(CE_GPU_ECORRUPT,
-                    fmt("Corruption: Matrix::Read: row_read.Dim() == %d expected, but %d found: %s", c,
-                        (int)row.size(), name.c_str()));
-      std::copy(row.begin(), row.end(), out->begin() + (size_t)i * c);
-    }
-    *rows = r;
-    *cols = c;
-    return CE_GPU_OK;
-  }
-};
-
-// Configuration::Read (src/configuration.cc:14-50): key = value, '#' comments,
-// keys case-insensitive, paths relative to the config file's directory.
-struct Config {
-  std::string file;
-  std::map<std::string, std::string> kv;
-  static std::string trim(const std::string &s) {
-    size_t a = 0, b = s.size();
-    while (a < b && isspace((unsigned char)s[a])) ++a;
-    while (b > a && isspace((unsigned char)s[b - 1])) --b;
-    return s.substr(a, b - a);
-  }
-  int read(const std::string &path) {
-    file = path;
-    std::ifstream in(path);
-    if (!in) return fail(CE_GPU_EIO, "IOError: Unable to open " + path);
-    std::string line;
-    while (std::getline(in, line)) {
-      while (!line.empty() && (line.back() == '\r' || line.back() == '\n')) line.pop_back();
-      line = trim(line);
-      if (line.empty() || line[0] == '#') continue;
-      size_t eq = line.find('=');
-      if (eq == std::string::npos || line.find('=', eq + 1) != std::string::npos)
-        return fail(CE_GPU_ECORRUPT, "Corruption: Unexpected line in " + path + ": " + line);
-      std::string k = trim(line.substr(0, eq)), v = trim(line.substr(eq + 1));
-      if (v.empty()) return fail(CE_GPU_ECORRUPT, "Corruption: Value cound not be empty: " + path);
-      std::transform(k.begin(), k.end(), k.begin(), [](unsigned char ch) { return (char)tolower(ch); });
-      kv[k] = v;
-    }
-    return CE_GPU_OK;
-  }
-  int get(const std::string &key, std::string *v) const {
-    auto it = kv.find(key);
-    if (it == kv.end())
-      return fail(CE_GPU_ECORRUPT, "Corruption: Unable to find key '" + key + "' in '" + file + "'");
-    *v = it->second;
-    return CE_GPU_OK;
-  }
-  int path(const std::string &key, std::string *v) const {
-    CE_TRY(get(key, v));
-    if ((*v)[0] == '/') return CE_GPU_OK;
-    size_t slash = file.rfind('/');
-    if (slash != std::string::npos) *v = file.substr(0, slash + 1) + *v;
-    return CE_GPU_OK;
-  }
-  int integer(const std::string &key, int *v) const {
-    std::string s;
-    CE_TRY(get(key, &s));
-    char *end = nullptr;
-    long x = strtol(s.c_str(), &end, 10);
-    if (end == s.c_str()) return fail(CE_GPU_ECORRUPT, "Corruption: not an integer: " + key);
-    *v = (int)x;
-    return CE_GPU_OK;
-  }
-};
-
-// ------------------------------------------------------------ nnet model --
-
-// Layer ids (src/nnet.h:21-30).
-enum LayerId { kLinear = 0, kReLU = 1, kNormalize = 2, kSoftmax = 3, kSplice = 6, kBatchNorm = 7,
-               kLogSoftmax = 8, kNarrow = 9 };
-
-struct RawLayer {
-  int id = -1;
-  std::vector<float> w, b, scale, offset;  // linear: w is in x out
-  int rows = 0, cols = 0;
-  std::vector<int32_t> idx;  // splice
-  int left = 0, right = 0;   // narrow
-};
-
-// Nnet::Read / ReadLayer (src/nnet.cc:221-293)
-static int read_nnet(Reader &rd, std::vector<RawLayer> *layers, int *hl, int *hr) {
-  const std::string &path = rd.name;
-  CE_TRY(rd.tag("NN02"));
-  int32_t l = 0, r = 0, n = 0;
-  CE_TRY(rd.i32(&l));
-  CE_TRY(rd.i32(&r));
-  CE_TRY(rd.i32(&n));
-  *hl = l;
-  *hr = r;
-  for (int i = 0; i < n; ++i) {
-    RawLayer L;
-    CE_TRY(rd.tag("LAY0"));
-    int32_t id = 0;
-    CE_TRY(rd.i32(&id));
-    L.id = id;
-    switch (id) {
-      case kLinear:
-        CE_TRY(rd.mat(&L.w, &L.rows, &L.cols));
-        CE_TRY(rd.vec(&L.b));
-        break;
-      case kReLU:
-      case kNormalize:
-      case kSoftmax:
-      case kLogSoftmax:
-        break;
-      case kSplice: {
-        int32_t cnt = 0;
-        CE_TRY(rd.i32(&cnt));
-        if (cnt < 0) return fail(CE_GPU_ECORRUPT, "Corruption: SpliceLayer: unexpected num_indcies");
-        L.idx.resize(cnt);
-        for (int k = 0; k < cnt; ++k) CE_TRY(rd.i32(&L.idx[k]));
-        break;
-      }
-      case kBatchNorm:
-        CE_TRY(rd.vec(&L.scale));
-        CE_TRY(rd.vec(&L.offset));
-        break;
-      case kNarrow:
-        CE_TRY(rd.i32(&L.left));
-        CE_TRY(rd.i32(&L.right));
-        break;
-      default:
-        return fail(CE_GPU_ECORRUPT, fmt("Corruption: read_layer: unexpected layer type: %d (%s)", id,
-                                         path.c_str()));
-    }
-    layers->push_back(std::move(L));
-  }
-  return CE_GPU_OK;
 }
 
 // Turns the layer list into fused device steps.  The reference's converter
@@ -676,7 +466,7 @@ using namespace catears;
 
 extern "C" {
 
-const char *ce_gpu_last_error(void) { return g_last_error.c_str(); }
+const char *ce_gpu_last_error(void) { return last_error(); }
 
 const char *ce_gpu_version(void) { return "catears-mi355x 0.4 (gfx950)"; }
 
@@ -1658,6 +1448,19 @@ int ce_gpu_model_load_mem(ce_gpu_ctx *ctx, const void *nnet, int64_t nbytes, con
   CE_TRY(read_program(ctx, rd, left_context, right_context, m.get()));
   if (h_prior) CE_TRY(set_prior(m.get(), h_prior, prior_dim));
   *out = m.release();
+  return CE_GPU_OK;
+}
+
+int ce_gpu_nnet_check_mem(const void *nnet, int64_t nbytes, int *num_layers, int *left, int *right) {
+  if (!nnet || nbytes <= 0) return fail(CE_GPU_EINVAL, "bad argument");
+  Reader rd;
+  CE_TRY(rd.open_mem(nnet, (size_t)nbytes, "<nnet image>"));
+  std::vector<RawLayer> layers;
+  int hl = 0, hr = 0;
+  CE_TRY(read_nnet(rd, &layers, &hl, &hr));
+  if (num_layers) *num_layers = (int)layers.size();
+  if (left) *left = hl;
+  if (right) *right = hr;
   return CE_GPU_OK;
 }
 

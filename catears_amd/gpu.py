@@ -32,7 +32,7 @@ ABI = [
     "ce_gpu_nnet_propagate_blocks", "ce_gpu_loglik_gather", "ce_gpu_loglik_columns",
     "ce_gpu_model_set_gemm", "ce_gpu_model_get_gemm", "ce_gpu_ctx_overflow", "ce_gpu_ctx_set_latency",
     "ce_gpu_fbank_s16", "ce_gpu_score_s16", "ce_gpu_ctx_set_fbank", "ce_gpu_sum_f64", "ce_gpu_ctx_set_wide_tiles",
-    "ce_gpu_sum_f64_many", "ce_gpu_trace_mark",
+    "ce_gpu_sum_f64_many", "ce_gpu_trace_mark", "ce_gpu_nnet_check_mem",
 ]
 
 # ce_gpu_model_set_gemm modes
@@ -90,6 +90,7 @@ def lib():
         "ce_gpu_gemm_u8u8i32": (ci, [vp, ci, ci, ci, vp, vp, vp, vp, vp]),
         "ce_gpu_profile_anchor": (ci, [ci, vp]),
         "ce_gpu_trace_mark": (ci, [ci, vp, ci]),
+        "ce_gpu_nnet_check_mem": (ci, [vp, i64, pi, pi, pi]),
         "ce_gpu_model_quantize": (ci, [vp, vp]),
         "ce_gpu_nnet_propagate_blocks": (ci, [vp, vp, vp, ci, ctypes.POINTER(ctypes.c_int32), ci, ci, vp]),
         "ce_gpu_ctx_profile_intervals": (ci, [vp, ci, vp, vp, ci, pi]),
@@ -286,6 +287,16 @@ class Model:
 def profile_anchor(device, stream):
     """Record the time origin for Context.profile_intervals on `stream`."""
     check(lib().ce_gpu_profile_anchor(device, ctypes.c_void_p(stream.cuda_stream)))
+
+
+def nnet_check(image):
+    """ce_gpu_nnet_check_mem: parse an NN02 image without a device; returns
+    (num_layers, left, right) or raises CatearsError with the reference's
+    message."""
+    buf = bytes(image)
+    n, l, r = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    check(lib().ce_gpu_nnet_check_mem(buf, len(buf), ctypes.byref(n), ctypes.byref(l), ctypes.byref(r)))
+    return n.value, l.value, r.value
 
 
 def trace_mark(device, stream, tag):

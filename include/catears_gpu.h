@@ -255,6 +255,16 @@ int ce_gpu_model_destroy(ce_gpu_model *m);
 int ce_gpu_model_load_mem(ce_gpu_ctx *ctx, const void *nnet, int64_t nbytes, const float *h_prior,
                           int prior_dim, int left_context, int right_context, ce_gpu_model **out);
 
+/* Nnet::Read (src/nnet.cc:221-293) without a device: parses an NN02 image
+ * exactly as ce_gpu_model_load_mem does -- CE_GPU_EIO "IOError: failed to
+ * read: ..." for a truncated image (also for a section whose declared length
+ * runs past the end, where the reference would first try to allocate it),
+ * CE_GPU_ECORRUPT with the reference's messages for a wrong tag, a VEC0
+ * section size, a MAT0 row width or an unknown layer type -- and reports the
+ * layer count and the header's left / right context (any pointer may be
+ * NULL).  Needs no GPU and touches none. */
+int ce_gpu_nnet_check_mem(const void *nnet, int64_t nbytes, int *num_layers, int *left, int *right);
+
 /* --------------------------------------------------------------- plan --- */
 
 /* Frames of one utterance of n samples: 0 if n < 400 else 1 + (n - 400) / 160
