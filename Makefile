@@ -117,6 +117,29 @@ $(COMPATTEST): tests/native/compat_test.cc $(wildcard $(HOST)/compat_src/*.cc) $
 	@mkdir -p $(dir $@)
 	$(CXX) -O1 -std=c++17 -Wall -I$(HOST)/compat -o $@ $< $(wildcard $(HOST)/compat_src/*.cc)
 
+# The same container layer and the model-file parsers under AddressSanitizer +
+# UndefinedBehaviorSanitizer (host code only; tests/test_dropin.py runs them
+# on the CPU): compat_test, and parse_fuzz over model_io.cc (the C-ABI's NN02 /
+# MAT0 / VEC0 / config readers) and the drop-in Nnet::Read, fed truncated and
+# corrupted images.  The drop-in nnet.cc links the product libraries for the
+# device calls it never makes here.
+SANFLAGS := -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=all
+COMPATASAN := build/bin/compat_test_asan
+FUZZASAN := build/bin/parse_fuzz_asan
+$(COMPATASAN): tests/native/compat_test.cc $(wildcard $(HOST)/compat_src/*.cc) $(wildcard $(HOST)/compat/*.h)
+	@mkdir -p $(dir $@)
+	$(CXX) $(SANFLAGS) -std=c++17 -Wall -I$(HOST)/compat -o $@ $< $(wildcard $(HOST)/compat_src/*.cc)
+$(FUZZASAN): tests/native/parse_fuzz.cc $(SRC)/model_io.cc $(SRC)/model_io.h $(HOST)/src/nnet.cc $(PKHDRS) $(LIB) \
+             $(wildcard $(HOST)/compat_src/*.cc)
+	@mkdir -p $(dir $@)
+	$(CXX) $(SANFLAGS) -std=c++17 -ffp-contract=off -D__HIP_PLATFORM_AMD__ -Wall $(PKINC) -I$(SRC) -o $@ \
+	    tests/native/parse_fuzz.cc $(SRC)/model_io.cc $(HOST)/src/nnet.cc $(HOST)/src/runtime.cc \
+	    $(HOST)/src/linalg.cc $(wildcard $(HOST)/compat_src/*.cc) \
+	    -Lcatears_amd/lib -lcatears_hip -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,$(CURDIR)/catears_amd/lib \
+	    -Wl,-rpath,/opt/rocm/lib
+sanitize: $(COMPATASAN) $(FUZZASAN)
+.PHONY: sanitize
+
 host: $(PKLIB) $(PKTEST) $(COMPATTEST)
 all: host
 .PHONY: host

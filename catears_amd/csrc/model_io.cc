@@ -108,16 +108,18 @@ int Reader::mat(std::vector<float> *out, int *rows, int *cols) {
   MIO_TRY(i32(&r));
   MIO_TRY(i32(&c));
   if (r < 0 || c < 0) return fail(CE_GPU_ECORRUPT, "Corruption: negative matrix shape in " + name);
-  // each row is a whole VEC0 section: 12 header bytes + 4 per element
-  MIO_TRY(need((int64_t)r * (12 + 4 * (int64_t)c)));
-  out->resize((size_t)r * c);
+  // The rows are appended as they are read rather than allocated from the
+  // header's shape, so the storage never outgrows the file and every error
+  // is the one the reference reports for the same bytes (a short row before
+  // the end: the row width; the end first: the truncated file).
+  out->clear();
   std::vector<float> row;
   for (int i = 0; i < r; ++i) {
     MIO_TRY(vec(&row));
     if ((int)row.size() != c)
       return fail(CE_GPU_ECORRUPT, fmt("Corruption: Matrix::Read: row_read.Dim() == %d expected, but %d found: %s",
                                        c, (int)row.size(), name.c_str()));
-    std::copy(row.begin(), row.end(), out->begin() + (size_t)i * c);
+    out->insert(out->end(), row.begin(), row.end());
   }
   *rows = r;
   *cols = c;

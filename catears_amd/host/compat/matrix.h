@@ -142,15 +142,23 @@ class Matrix : public MatrixBase<Real> {
     PK_CHECK_STATUS(fd->ReadValue<int32_t>(&rows));
     PK_CHECK_STATUS(fd->ReadValue<int32_t>(&cols));
     if (rows < 0 || cols < 0) return Status::Corruption("negative matrix shape in " + fd->filename());
-    Resize(rows, cols, kUndefined);
+    // The rows are collected as they are read and the matrix sized after the
+    // last one, so storage never outgrows the file (a corrupt shape in the
+    // billions fails as the truncated file it is, where the reference would
+    // abort in posix_memalign) and every error is the reference's for the
+    // same bytes.
+    std::vector<Real> rows_read;
     Vector<Real> row;
     for (int r = 0; r < rows; ++r) {
       PK_CHECK_STATUS(row.Read(fd));
       if (row.Dim() != cols)
         return Status::Corruption(util::Format("Matrix::Read: row_read.Dim() == {} expected, but {} found: {}",
                                                cols, row.Dim(), fd->filename()));
-      this->Row(r).CopyFromVec(row);
+      rows_read.insert(rows_read.end(), row.Data(), row.Data() + cols);
     }
+    Resize(rows, cols, kUndefined);
+    for (int r = 0; r < rows; ++r)
+      if (cols) memcpy(this->Row(r).Data(), rows_read.data() + (size_t)r * cols, sizeof(Real) * cols);
     return Status::OK();
   }
 

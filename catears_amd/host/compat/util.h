@@ -76,6 +76,11 @@ class ReadableFile {
   Status ReadValue(T *data) {
     return Read(data, sizeof(T));
   }
+  // Fails as a truncated file ("failed to read: <file>") unless `bytes`
+  // more bytes are left: a section length read from a corrupt header is
+  // checked before anything is allocated for it (the reference would try
+  // the allocation and abort).  A borrowed stream of unknown size passes.
+  Status Need(int64_t bytes);
   bool ReadLine(std::string *line, Status *status);
   bool Eof() const;
   void Close();

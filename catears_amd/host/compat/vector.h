@@ -161,6 +161,7 @@ class Vector : public VectorBase<Real> {
     if (dim < 0 || (int64_t)dim * (int64_t)sizeof(Real) + 4 != section)
       return Status::Corruption(util::Format("section_size = {} * {} + 4 expected, but {} found: {}", dim,
                                              sizeof(Real), section, fd->filename()));
+    PK_CHECK_STATUS(fd->Need((int64_t)dim * (int64_t)sizeof(Real)));
     Resize(dim, kUndefined);
     if (dim) PK_CHECK_STATUS(fd->Read(this->data_, (int)(dim * sizeof(Real))));
     return Status::OK();

@@ -6,6 +6,7 @@
 #include <ctype.h>
 #include <errno.h>
 #include <stdlib.h>
+#include <sys/stat.h>
 
 #include <algorithm>
 
@@ -78,6 +79,20 @@ Status ReadableFile::ReadAndVerifyString(const std::string &expected) {
   if (got != expected)
     return Status::Corruption(
         Format("ReadAndVerifyString: '{}' expected but '{}' found in {}", expected, got, filename_));
+  return Status::OK();
+}
+
+Status ReadableFile::Need(int64_t bytes) {
+  if (!fd_) return Status::IOError(Format("failed to read: {}", filename_));
+  int64_t size = file_size_;
+  if (!owned_) {
+    struct stat st;
+    if (fstat(fileno(fd_), &st) != 0 || !S_ISREG(st.st_mode)) return Status::OK();
+    size = st.st_size;
+  }
+  const long at = ftell(fd_);
+  if (at < 0) return Status::OK();
+  if (bytes < 0 || bytes > size - at) return Status::IOError(Format("failed to read: {}", filename_));
   return Status::OK();
 }
 

@@ -105,6 +105,48 @@ def test_compat_container_layer(tmp_path):
     assert r.returncode == 0 and "PASSED" in r.stdout, r.stdout + r.stderr
 
 
+def test_parsers_under_address_and_ub_sanitizers(tmp_path):
+    """the host code under ASan + UBSan.  The compat container
+    layer (compat_test) and the model-file parsers -- model_io.cc's NN02 /
+    MAT0 / VEC0 readers behind ce_gpu_model_load_mem, and the drop-in
+    Nnet::Read -- fed a valid image, every truncation of it, the reference's
+    corruption cases (its messages), sections declared billions of bytes
+    long and 20 000 seeded random corruptions (tests/native/parse_fuzz.cc):
+    no sanitizer report, both parsers agree on every input."""
+    subprocess.check_call(["make", "-C", ROOT, "-s", "sanitize"], stdout=subprocess.DEVNULL)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:halt_on_error=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    for exe, args in (("compat_test_asan", []), ("parse_fuzz_asan", ["20000"])):
+        r = subprocess.run([os.path.join(ROOT, "build", "bin", exe), str(tmp_path)] + args, capture_output=True,
+                           text=True, env=env, timeout=300)
+        assert r.returncode == 0 and "PASSED" in r.stdout, exe + "\n" + r.stdout[-3000:] + r.stderr[-3000:]
+        assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr[-3000:]
+
+
+def test_nnet_check_mem_without_a_device(tmp_path):
+    """ce_gpu_nnet_check_mem parses an NN02 image on a machine without a GPU:
+    the layer count and context of a valid image, the reference's messages
+    for corrupt ones, the truncated-file error for a section declared longer
+    than the image."""
+    from catears_amd import formats, gpu, synth
+    layers, left, right, _ = synth.tdnn_layers(256, 512, seed=3)
+    img = bytearray(formats.nnet_bytes(layers, left, right))
+    (tmp_path / "m.nnet").write_bytes(bytes(img))
+    want, wl, wr = formats.read_nnet(str(tmp_path / "m.nnet"))
+    assert gpu.nnet_check(img) == (len(want), wl, wr)
+    bad = bytearray(img)
+    bad[3:4] = b"3"
+    with pytest.raises(gpu.CatearsError, match="ReadAndVerifyString: 'NN02' expected but 'NN03' found"):
+        gpu.nnet_check(bad)
+    with pytest.raises(gpu.CatearsError, match="IOError: failed to read"):
+        gpu.nnet_check(img[:len(img) // 2])
+    # the first layer's count field set to 2^31 - 1: refused before any allocation
+    huge = bytearray(img)
+    huge[24:28] = (0x7fffffff).to_bytes(4, "little")
+    with pytest.raises(gpu.CatearsError):
+        gpu.nnet_check(huge)
+
+
 # ------------------------------------------------------------ GPU checks --
 
 def _run(*args, env=None):
