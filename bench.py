@@ -313,7 +313,7 @@ def pmc_valu(kernel):
             if kernel_match(name, base + "*") and tmpl.split("*")[0] in name:
                 return dict(v, source=os.path.relpath(f, ROOT),
                             definition="tools/pmc_valu.py: valu_active_per_simd = SQ_ACTIVE_INST_VALU / "
-                                       "(4 SQ_BUSY_CU_CYCLES); valu_busy_amd = AMD's VALUBusy; valu_issue_2cyc = "
+                                       "SQ_BUSY_CU_CYCLES; valu_busy_amd = AMD's VALUBusy; valu_issue_2cyc = "
                                        "SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x cycles); wave_* = fractions "
                                        "of SQ_WAVE_CYCLES")
     return None
@@ -881,7 +881,9 @@ def verify_serial(args, kept, ctx, model, plan, pcm, gstats, U, pool):
     from catears_amd import gpu
     torch.cuda.synchronize()
     ctx.set_fbank(args.fbank)  # the front contexts' fbank mode (the re-score runs on one context)
-    raw = torch.empty_like(kept[0][0])
+    if not kept:
+        return {"batches": 0, "differing": 0, "detail": []}
+    raw = torch.empty_like(kept[min(kept)][0])  # step 0 is not kept where rank 0 scores part of the steps
     norm = torch.empty_like(raw) if gstats is not None else raw
     out = torch.empty((plan.total_frames, model.num_pdfs), dtype=torch.float32, device="cuda")
     bad = []

@@ -11,10 +11,13 @@ SQ_WAVE_CYCLES and SQ_BUSY_CU_CYCLES count quad-cycles (4 shader cycles),
 summed over waves / CUs; GRBM_GUI_ACTIVE counts cycles summed over the 8
 XCDs.  Per kernel, over its dispatches:
 
-  valu_active_per_simd = SQ_ACTIVE_INST_VALU / (4 x SQ_BUSY_CU_CYCLES)
+  valu_active_per_simd = SQ_ACTIVE_INST_VALU / SQ_BUSY_CU_CYCLES
       the cycles in which a wave of the SIMD was executing VALU work, per
-      busy cycle of the SIMD (the VERDICT r5 ratio); above 1 means the VALU
-      work of several waves of one SIMD overlaps in time
+      busy cycle of the SIMD (the VERDICT r5 ratio).  SQ_BUSY_CU_CYCLES is
+      summed over a CU's 4 SIMDs in quad-cycles, i.e. it counts the CU's busy
+      cycles (cu_busy below reads 0.92 on the C2 launch, not 3.7).  Above 1
+      means the VALU work of several waves of one SIMD overlaps in time: it is
+      per-wave occupancy, not the pipe's
   valu_busy_amd = SQ_ACTIVE_INST_VALU / (CUs x GRBM_GUI_ACTIVE / 8)
       AMD's own derived `VALUBusy` (counter_defs.yaml), the same quotient
       over the dispatch's cycles instead of the CUs' busy cycles
@@ -65,10 +68,10 @@ def main():
         wc = a["SQ_WAVE_CYCLES"]
         res[k] = {
             "dispatches": int(a["n"]),
-            "valu_active_per_simd": round(a["SQ_ACTIVE_INST_VALU"] / (4 * a["SQ_BUSY_CU_CYCLES"]), 4),
+            "valu_active_per_simd": round(a["SQ_ACTIVE_INST_VALU"] / a["SQ_BUSY_CU_CYCLES"], 4),
             "valu_busy_amd": round(a["SQ_ACTIVE_INST_VALU"] / (CUS * cyc), 4),
             "valu_issue_2cyc": round(a["SQ_INSTS_VALU"] * 2 / (SIMDS * cyc), 4),
-            "cu_busy": round(4 * a["SQ_BUSY_CU_CYCLES"] / (CUS * cyc), 4),
+            "cu_busy": round(a["SQ_BUSY_CU_CYCLES"] / (CUS * cyc), 4),
             "wave_active": round(a["SQ_ACTIVE_INST_ANY"] / wc, 4),
             "wave_issue_stall": round(a["SQ_WAIT_INST_ANY"] / wc, 4),
             "wave_parked": round(a["SQ_WAIT_ANY"] / wc, 4),

@@ -75,7 +75,7 @@ def main():
     ap.add_argument("title", nargs="*")
     ap.add_argument("--window", action="store_true")
     ap.add_argument("--check")
-    args = ap.parse_args()
+    args = ap.parse_intermixed_args()
     rows = [r for r in read_trace(args.trace)]
     win_us = None
     if args.window:
