@@ -290,6 +290,34 @@ def pmc_traffic(kernel, workload="c3"):
     return round(sum(v["hbm_bytes_per_launch"] * v["dispatches"] for v in hits) / n), os.path.relpath(files[-1], ROOT)
 
 
+TDNN_S_GEMMS = ((200, 1024),) + ((3072, 1024),) * 4 + ((1024, 1024), (1024, 3456))  # (K, N) of layers 1-7
+
+
+def pmc_traffic_layers(rows):
+    """Per-layer PMC bytes of the C3 GEMM launches (tools/pmc_traffic.py
+    --layers 7 over the serial PMC passes of this bench) beside each layer's
+    algorithmic bytes: fp32 activations once per row and segment (4 rows K),
+    the weights at 4 B (the fp32 matrix) and at 6 B (the bf16x6 fragment
+    image the kernel reads), fp32 outputs (4 rows N).  None without the file."""
+    import glob
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json"))
+                   if not re.search(r"_c\d_pmc_traffic\.json$", f))
+    for f in reversed(files):
+        data = json.load(open(f))
+        if "gemm_layers" not in data:
+            continue
+        out = []
+        for L, (k, n) in zip(data["gemm_layers"], TDNN_S_GEMMS):
+            alg = 4 * rows * k + 4 * k * n + 4 * rows * n
+            alg6 = alg + 2 * k * n
+            out.append({"layer": L["layer"], "k": k, "n": n, "pmc_bytes": L["hbm_bytes_per_launch"],
+                        "algorithmic_bytes": alg, "algorithmic_bytes_fragment_image": alg6,
+                        "pmc_over_algorithmic": round(L["hbm_bytes_per_launch"] / alg, 3),
+                        "pmc_over_fragment_image": round(L["hbm_bytes_per_launch"] / alg6, 3)})
+        return {"source": os.path.relpath(f, ROOT), "rows": rows, "layers": out}
+    return None
+
+
 def sink_share_default(world):
     """Rank 0's share of the scoring at `world` ranks on RCCL:
     from the one-GPU rehearsals, rank 0's step grows about 0.034 ms per peer
@@ -1332,6 +1360,7 @@ def main(argv=None):
                         "flops_per_launch": flops_per_launch,
                         "pmc_mfma_util": pmc_mfma(kname),
                         "algorithmic_bytes_per_launch": split_algorithmic_bytes(plan.max_chunk_rows, eb),
+                        "traffic_per_layer": pmc_traffic_layers(plan.max_chunk_rows) if f32in else None,
                         "traffic_scope": ("PMC bytes per launch averaged over all 7 layers (fp32 operands)" if f32in else
                                           "PMC bytes per hidden-layer launch (split-output instantiation, layers "
                                           "1-6); algorithmic bytes of the same launches: "

@@ -935,6 +935,196 @@ __global__ __launch_bounds__(C::NT, 512 / C::NT) void gemm_bf16x6d_kernel(X6Args
   x6_epilogue<TW, TF, OUT16>(p, acc, n0 + ww * TW * 16, f0 + frow, lane);
 }
 
+// One wave per SIMD (gemm_bf16x6w_kernel): 4 waves per block, each with up
+// to 512 registers (the 256 accumulators of a 128 x 128 wave tile live in
+// AGPRs), so every operand fragment feeds twice the products of the 8-wave
+// kernel.  Block BW units x BF frames as WGW x WGF waves of TW x TF 16 x 16
+// fragments.  At 512 x 128 (4 x 1 waves of 128 units x 128 frames), per
+// output element and K-tile this halves the weight fragments loaded (each is
+// loaded by exactly one wave), the activation fragments read from LDS (read
+// by 4 waves for 128 frames x 512 units instead of 4 for 128 x 256) and the
+// activation loads + split + LDS writes (one block covers 512 units) -- the
+// bytes and VALU that cost clock at the chip's power cap (DESIGN.md §8 r5,
+// r05z5 ablations).
+// Per K-tile the wave runs its TW unit blocks in order; unit block i takes
+// the TF frame blocks with the six products in gemm_bf16x6d_kernel's order
+// per accumulator (a0b0, a0b1, a1b0, a1b1, a0b2, a2b0; K-tiles in order), so
+// the results are bit-identical to it.
+//   * weights: a ring of 4 unit-block buffers (3 planes each), each loaded
+//     3 unit blocks (3 x 6 TF MFMAs) ahead of its use, straight from the
+//     fragment image to registers, across K-tile boundaries;
+//   * activations: the TF x 3 plane fragments of the K-tile stay in registers
+//     for all TW unit blocks; in the last unit block each frame block's
+//     fragments are replaced by the next K-tile's as soon as its six
+//     products are issued;
+//   * unit block 0: the next K-tile's activation rows (loaded one K-tile
+//     ago) are split into the free LDS stage and the one after is loaded;
+//     after unit block TW/2 - 1: lgkmcnt(0) and the block barrier (RAW for
+//     the next K-tile's stage; WAR: a stage is rewritten one K-tile after
+//     the barrier that follows its last reads).
+template <int BW_, int BF_, int WGW_, int WGF_>
+struct W6Cfg {
+  static constexpr int BW = BW_, BF = BF_, WGW = WGW_, WGF = WGF_;
+  static constexpr int NW = WGW * WGF, NT = 64 * NW;
+  static constexpr int TW = BW / WGW / 16, TF = BF / WGF / 16;  // 16 x 16 fragments per wave
+  static_assert(TW * WGW * 16 == BW && TF * WGF * 16 == BF, "bad one-wave-per-SIMD tile");
+};
+
+// SG: pin the interleave with sched_group_barrier -- the split + LDS writes of
+// unit block 0 between its MFMAs (1 MFMA : 2 VALU), and in the last unit
+// block each frame block's three fragment reads right after its six MFMAs
+// (the compiler otherwise issues the split as one VALU block ahead of the
+// MFMAs and sinks the reads to the end of the K-tile).
+// RING: unit-block weight buffers in flight (RING - 1 unit blocks ahead).
+// NW = 8 (two waves per SIMD, 256 registers each) is the same schedule with
+// the accumulators of a 128 x 64 wave tile in AGPRs.
+template <class C, bool SG = false, int RING = 4>
+__global__ __launch_bounds__(C::NT, C::NW / 4) void gemm_bf16x6w_kernel(X6Args p) {
+  constexpr int BF = C::BF, TW = C::TW, TF = C::TF, NT = C::NT;
+  static_assert(C::NW == 4 || C::NW == 8, "one or two waves per SIMD");
+  static_assert(TW % RING == 0, "a ring of unit-block weight buffers that divides the unit blocks");
+  constexpr int RQ = BF / (NT / 4);  // activation rows per thread per K-tile
+  static_assert(RQ >= 1 && RQ * (NT / 4) == BF, "whole activation rows per thread");
+  constexpr int ASTAGE = 3 * BF * 64;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * ASTAGE];
+  auto swz = [](int row) { return ((row >> 3) & 1) << 1; };
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  typedef const __attribute__((address_space(1))) f32x4v gvec;
+  typedef const __attribute__((address_space(1))) bf16x8 gfrag;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ww = wave / C::WGF, wf = wave % C::WGF;
+  int tm, tn;
+  tile_of(blockIdx.x, p.tiles_m, p.tiles_n, p.group, &tm, &tn);
+  const int f0 = tm * BF, n0 = tn * C::BW;
+  const int prow = tid >> 2, pch = tid & 3;
+  const int ktiles = p.kpad / 32;
+
+  // the wave's unit block i, K-tile kt, plane pl: fragment
+  // ((ub0 + i) * wd_kt + kt) * 3 + pl of the image, lane's 16 bytes
+  gfrag *wbase = (gfrag *)(p.wd + ((size_t)((n0 >> 4) + ww * TW) * p.wd_kt * 3 * 64 + lane) * 8);
+  bf16x8 wa[RING][3];
+  auto load_w = [&](int kt, int i, int buf) {
+    kt = min(kt, ktiles - 1);
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) wa[buf][pl] = wbase[((size_t)(i * p.wd_kt + kt) * 3 + pl) * 64];
+  };
+  f32x4v rx0[RQ], rx1[RQ];
+  auto load_x = [&](int kt) {
+    kt = min(kt, ktiles - 1);
+    const int k0 = kt * 32;
+    const int seg = k0 / p.din, col0 = k0 - seg * p.din;
+    const int shift = (int)(signed char)(p.off_packed >> (8 * seg));
+    gvec *xb = (gvec *)(p.xf + col0 + 8 * pch);
+#pragma unroll
+    for (int q = 0; q < RQ; ++q) {
+      const int src = clampi(f0 + prow + q * (NT / 4) + shift, 0, p.m - 1);
+      const uint32_t o = (uint32_t)(src * p.ldx) / 4;
+      rx0[q] = xb[o];
+      rx1[q] = xb[o + 1];
+    }
+  };
+  auto put = [&](char *st) {
+#pragma unroll
+    for (int q = 0; q < RQ; ++q) {
+      const Planes2 q0 = split3_pair(rx0[q].x, rx0[q].y), q1 = split3_pair(rx0[q].z, rx0[q].w);
+      const Planes2 q2 = split3_pair(rx1[q].x, rx1[q].y), q3 = split3_pair(rx1[q].z, rx1[q].w);
+      const int row = prow + q * (NT / 4);
+      const int off = row * 64 + ((pch ^ swz(row)) * 16);
+      *reinterpret_cast<u32x4 *>(st + off) = u32x4{q0.h, q1.h, q2.h, q3.h};
+      *reinterpret_cast<u32x4 *>(st + BF * 64 + off) = u32x4{q0.m, q1.m, q2.m, q3.m};
+      *reinterpret_cast<u32x4 *>(st + 2 * BF * 64 + off) = u32x4{q0.l, q1.l, q2.l, q3.l};
+    }
+  };
+  const int foff = (lane & 15) * 64 + (((lane >> 4) ^ (((lane >> 3) & 1) << 1)) * 16);
+  const int frow = wf * TF * 16;
+  auto frag = [&](const char *st, int pl, int j) {
+    return *reinterpret_cast<const bf16x8 *>(st + (pl * BF + frow + j * 16) * 64 + foff);
+  };
+
+  f32x4 acc[TW][TF];
+#pragma unroll
+  for (int i = 0; i < TW; ++i)
+#pragma unroll
+    for (int j = 0; j < TF; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  bf16x8 b0[TF], b1[TF], b2[TF];
+
+  load_x(0);
+#pragma unroll
+  for (int i = 0; i < RING - 1; ++i) load_w(0, i, i);
+  put(smem);
+  load_x(1);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int j = 0; j < TF; ++j) {
+    b0[j] = frag(smem, 0, j);
+    b1[j] = frag(smem, 1, j);
+    b2[j] = frag(smem, 2, j);
+  }
+
+  for (int kt = 0; kt < ktiles; ++kt) {
+    char *sn = smem + ((kt + 1) & 1) * ASTAGE;
+#pragma unroll
+    for (int i = 0; i < TW; ++i) {
+      // the weights three unit blocks ahead (the next K-tile's first ones
+      // from unit block TW - 3 on)
+      load_w(kt + (i + RING - 1) / TW, (i + RING - 1) % TW, (i + RING - 1) % RING);
+      if (i == 0) {
+        if constexpr (!SG) {
+          put(sn);
+          load_x(kt + 2);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (SG) {
+        if (i == 0) {
+          put(sn);
+          load_x(kt + 2);
+#pragma unroll
+          for (int g = 0; g < 6 * TF; ++g) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // 2 VALU
+            if (g % 4 == 3) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // an LDS write
+          }
+        }
+      }
+      constexpr int u = 0;  // (the ring slot is i % RING, a constant once unrolled)
+#pragma unroll
+      for (int j = 0; j < TF; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[i % RING][u], b0[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[i % RING][u], b1[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[i % RING][u + 1], b0[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[i % RING][u + 1], b1[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[i % RING][u], b2[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[i % RING][u + 2], b0[j], acc[i][j], 0, 0, 0);
+        if (i == TW - 1) {  // frame block j is done for this K-tile: the next one's fragments
+          b0[j] = frag(sn, 0, j);
+          b1[j] = frag(sn, 1, j);
+          b2[j] = frag(sn, 2, j);
+        }
+      }
+      if constexpr (SG) {
+        if (i == TW - 1) {
+#pragma unroll
+          for (int j = 0; j < TF; ++j) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);  // frame block j's six MFMAs
+            __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);  // its next fragments
+          }
+        }
+      }
+      if (i == TW / 2 - 1) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // the clamped tail prefetches
+  x6_epilogue<TW, TF, false>(p, acc, n0 + ww * TW * 16, f0 + frow, lane);
+}
+
 #ifdef CATEARS_EXPERIMENTS
 // Register-direct schedule (variant 400): both operands go straight from
 // L2 / L1 to registers -- the weights from the MFMA-fragment image as in
@@ -1281,6 +1471,17 @@ int launch_d(hipStream_t s, X6Args p) {
   return CE_GPU_OK;
 }
 
+// the one-wave-per-SIMD kernel; false when the fragment image does not cover
+// the last unit tile (the image pads units to a multiple of 256)
+template <class C, bool SG = false, int RING = 4>
+bool launch_w(hipStream_t s, X6Args p) {
+  p.tiles_n = (p.n + C::BW - 1) / C::BW;
+  p.tiles_m = (p.m + C::BF - 1) / C::BF;
+  if ((p.n + 255) / 256 * 256 < p.tiles_n * C::BW) return false;
+  hipLaunchKernelGGL((gemm_bf16x6w_kernel<C, SG, RING>), dim3(p.tiles_m * p.tiles_n), dim3(C::NT), 0, s, p);
+  return true;
+}
+
 template <class C, int NPV>
 int launch_ws(hipStream_t s, X6Args p) {
   p.tiles_n = (p.n + C::BW - 1) / C::BW;
@@ -1461,6 +1662,35 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
         if (x6_variant() == 334) return launch_d<X6Cfg<kX6DirUnits, 128, 4, 2, 2>, 0, 4>(s, p);
         if (x6_variant() == 335) return launch_d<X6Cfg<kX6DirUnits, 128, 4, 2, 2>, 0, 5>(s, p);
         return launch_d<X6Cfg<kX6DirUnits, 128, 4, 2, 2>, 0, 2>(s, p);
+#endif
+#if defined(CATEARS_EXPERIMENTS) || defined(CATEARS_X6W)
+      case 500:  // one wave per SIMD: 512 x 128 tiles, 4 waves of 128 units x 128 frames
+      case 501:  // 512 x 64, 4 waves of 128 x 64
+      case 502:  // 256 x 128, 4 waves of 64 x 128
+      case 503:    // 256 x 256, 2 x 2 waves of 128 x 128
+      case 504:    // 500 with the interleave pinned (sched_group_barrier)
+      case 505:    // 501 with the interleave pinned
+      case 506:    // 505 with the weights 7 unit blocks ahead (a ring of 8)
+      case 507:    // 502 (256 x 128) with the interleave pinned and a ring of 4
+      case 508: {  // 512 x 128 as 8 waves (two per SIMD) of 128 units x 64 frames, pinned, ring of 4
+        if (!a.wd || a.wd_kt * 32 < a.kpad) return fail(CE_GPU_EINVAL, "variants 500-503 need the weight fragment image");
+        if (first || a.wide) return launch_d<X6Cfg<128, 128, 2, 4, 2>>(s, p);
+        const int v = x6_variant();
+        const bool ok = v == 500   ? launch_w<W6Cfg<512, 128, 4, 1>>(s, p)
+                        : v == 504 ? launch_w<W6Cfg<512, 128, 4, 1>, true>(s, p)
+                        : v == 505 ? launch_w<W6Cfg<512, 64, 4, 1>, true>(s, p)
+                        : v == 506 ? launch_w<W6Cfg<512, 64, 4, 1>, true, 8>(s, p)
+                        : v == 507 ? launch_w<W6Cfg<256, 128, 4, 1>, true>(s, p)
+                        : v == 508 ? launch_w<W6Cfg<512, 128, 4, 2>, true>(s, p)
+                        : v == 501 ? launch_w<W6Cfg<512, 64, 4, 1>>(s, p)
+                        : v == 502 ? launch_w<W6Cfg<256, 128, 4, 1>>(s, p)
+                                   : launch_w<W6Cfg<256, 256, 2, 2>>(s, p);
+        if (!ok) return launch_d<X6Cfg<kX6DirUnits, 128, 4, 2, 2>>(s, p);
+        CE_HIP(hipGetLastError());
+        return CE_GPU_OK;
+      }
+#endif
+#ifdef CATEARS_EXPERIMENTS
       case 42:  // round-1 default: split of tile kt+1, then the MFMAs of tile kt
         return launch_f<X6Cfg<128, 256, 2, 4, 2>>(s, p);
       case 55:  // MFMAs of tile kt first, the split interleaved by the compiler

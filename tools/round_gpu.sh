@@ -25,7 +25,7 @@ for grp in FETCH_SIZE WRITE_SIZE; do
       > "$OUT/pmc$i.log" 2>&1 || { echo "pmc pass $i failed"; tail -20 "$OUT/pmc$i.log"; exit 1; }
   echo "pmc pass $i ok: $grp"
 done
-python "$R/tools/pmc_traffic.py" "$OUT/pmc1" "$OUT/pmc2" "$OUT/pmc_traffic.json"
+python "$R/tools/pmc_traffic.py" "$OUT/pmc1" "$OUT/pmc2" "$OUT/pmc_traffic.json" --layers 7
 timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "gemm_" \
     --output-format csv -d "$OUT/pmc3" -o run -- \
     python "$R/bench.py" --steps 4 --warmup 1 --no-cpu-baseline --no-profile --serial \
