@@ -28,13 +28,37 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# Hardware queues per process (HIP default 4): the pipeline's one front and
-# three nnet streams get one each.  Set before torch initialises HIP.
-# (measured: 8 queues with two front streams cost 5-6 % against the default
-# 4 with one; kept as an experiment knob, CATEARS_HW_QUEUES)
-HW_QUEUES = int(os.environ.get("CATEARS_HW_QUEUES", "4"))
+
+
+def default_back_streams(workload):
+    """nnet streams per process when --back-streams is not given: 8 for C3,
+    whose default GEMM (512 x 128 tiles, 64 blocks per hidden layer) needs
+    more batches in flight to fill the chip (profiles/r06f_driver_abba.txt:
+    8 streams + the last batch on wide tiles +2.5 % at the driver's flags
+    over the 256 x 128 kernel on 3); 3 for the other workloads."""
+    return 8 if workload == "c3" else 3
+
+
+def _early_arg(argv, name, default):
+    """The value of `--name X` / `--name=X` in argv, before argparse runs (the
+    hardware queue count must be set before torch initialises HIP)."""
+    for i, a in enumerate(argv):
+        if a == name and i + 1 < len(argv):
+            return argv[i + 1]
+        if a.startswith(name + "="):
+            return a.split("=", 1)[1]
+    return default
+
+
+# Hardware queues per process (HIP default 4): one per stream of the
+# pipeline -- the front stream, the nnet streams and the gather's
+# communication stream -- so no two streams share a queue.  Set before torch
+# initialises HIP.  (Measured, round 4: 8 queues with two front streams cost
+# 5-6 % against 4 with one; CATEARS_HW_QUEUES overrides.)
+_NB_EARLY = int(_early_arg(sys.argv, "--back-streams", default_back_streams(_early_arg(sys.argv, "--workload", "c3"))))
+HW_QUEUES = int(os.environ.get("CATEARS_HW_QUEUES", str(max(4, _NB_EARLY + 2))))
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < HW_QUEUES:
-    os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
+    os.environ["GPU_MAX_HW_QUEUES"] = str(min(HW_QUEUES, 32))
 
 FLOPS_PER_FRAME = 2 * (200 * 1024 + 4 * 3072 * 1024 + 1024 * 1024 + 1024 * 3456)  # 34,750,464
 # FLOPs per output frame of the GEMMs timed as CE_GPU_PROF_GEMM (all but layer 1)
@@ -120,10 +144,10 @@ def parse(argv=None):
                          "the library's (bf16x6: three exact bf16 planes, six products, fp32 GEMM)")
     ap.add_argument("--front-streams", type=int, default=1,
                     help="fbank + CMVN streams; consecutive batches alternate between them")
-    ap.add_argument("--wide-tiles", choices=["none", "last", "ends"], default="none",
+    ap.add_argument("--wide-tiles", choices=["none", "last", "ends"], default=None,
                     help="c3: score the last (or the first and the last) batch of each run of steps on 128 x 128 "
-                         "bf16x6 tiles (ce_gpu_ctx_set_wide_tiles: all CUs per launch while the pipeline fills or "
-                         "drains); same bits")
+                         "bf16x6 tiles (ce_gpu_ctx_set_wide_tiles: all CUs per launch while the pipeline drains); "
+                         "same bits.  Default: last for c3, none otherwise")
     ap.add_argument("--sink-share", type=float, default=None,
                     help="c3 / c4, N > 1: the fraction of steps (c4: of the corpus share) rank 0 scores a batch "
                          "of its own (it also receives and folds every peer's rows).  Default on RCCL: "
@@ -141,10 +165,15 @@ def parse(argv=None):
     ap.add_argument("--launch-check", action="store_true",
                     help="tests only: start and check the N ranks (self-launch, world size, gloo process group) "
                          "and print a line with n_gpus and the ranks seen, without touching a GPU")
-    ap.add_argument("--back-streams", type=int, default=3,
+    ap.add_argument("--back-streams", type=int, default=None,
                     help="nnet streams; consecutive batches alternate between them so one batch's "
-                         "wave-quantisation tail overlaps the next batch's layers")
-    return ap.parse_args(argv)
+                         "wave-quantisation tail overlaps the next batch's layers (default: 8 for c3, 3 otherwise)")
+    args = ap.parse_args(argv)
+    if args.back_streams is None:
+        args.back_streams = default_back_streams(args.workload)
+    if args.wide_tiles is None:
+        args.wide_tiles = "last" if args.workload == "c3" else "none"
+    return args
 
 
 def usable_cores():

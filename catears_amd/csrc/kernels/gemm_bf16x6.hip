@@ -1609,8 +1609,9 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
   }
   if (f32in) {
     switch (x6_variant()) {
-      case 0:
-      case 300:  // direct weights (the default when the model carries the fragment image)
+      case 0:    // the default (round 6): direct weights, the layers after the first on 512 x 128
+                 // tiles of 8 waves of 128 units x 64 frames (gemm_bf16x6w_kernel, variant 508)
+      case 300:  // direct weights on 256 x 128 tiles (gemm_bf16x6d_kernel, the rounds 3-5 default)
         if (a.wd) {
           if (a.wd_kt * 32 < a.kpad || (reinterpret_cast<uintptr_t>(a.wd) & 15))
             return fail(CE_GPU_EINVAL, "gemm_bf16x6: weight fragment image does not cover K");
@@ -1619,6 +1620,15 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
           // layer so with ce_gpu_ctx_set_wide_tiles (a batch scored while
           // no other is in flight then fills all CUs)
           if (a.wide || (first && x6_first_tile() == 128)) return launch_d<X6Cfg<128, 128, 2, 4, 2>>(s, p);
+          // 512-unit tiles: each block splits and stages its activation
+          // rows once for 512 units and each wave reads its B fragments once
+          // for 128 units -- half the activation path and LDS reads per
+          // product of 256 x 128; falls back when the
+          // fragment image (units padded to 256) does not cover the last tile
+          if (x6_variant() == 0 && !first && launch_w<W6Cfg<512, 128, 4, 2>, true>(s, p)) {
+            CE_HIP(hipGetLastError());
+            return CE_GPU_OK;
+          }
           return launch_d<X6Cfg<kX6DirUnits, 128, 4, 2, 2>>(s, p);
         }
         [[fallthrough]];

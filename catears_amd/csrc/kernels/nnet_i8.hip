@@ -710,7 +710,14 @@ __device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t r, int8_t *lds,
 //     the stage tile kt used, first reads of tile kt + 1) sits after tile
 //     kt's last MFMAs are issued, so the barrier's wait overlaps them.
 // int32 accumulation is exact, so any product order gives the same bits.
-template <int BM, int BN, int STAGES, int WGM, int WGN>
+// STAG: waves NW/2 .. NW-1 (the second wave of every SIMD) run two k-steps
+// behind the first half: their ks 0-1 of tile 0 before the loop, then per
+// K-tile ks 2-3 of tile kt, the hand-off, ks 0-1 of tile kt+1.  The
+// barriers, and so the stage protocol, are unchanged (a wave reaches tile
+// kt's hand-off only after all its reads of tile kt); the two waves of a
+// SIMD then read fragments while the other one multiplies
+// (MI355X_MICROARCH.md, "try a stagger").  Exact int32: same bits.
+template <int BM, int BN, int STAGES, int WGM, int WGN, bool STAG = false>
 __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_i8_pipe_kernel(I8Args p) {
   static_assert(STAGES == 3, "tile kt + 3 refills tile kt's stage");
   constexpr int NW = WGM * WGN, BKB = 128, CH = BKB / 16;
@@ -804,6 +811,39 @@ __global__ __launch_bounds__(64 * WGM * WGN, 1) void gemm_i8_pipe_kernel(I8Args 
   __builtin_amdgcn_s_barrier();
   if (STAGES - 1 < ktiles) issue(STAGES - 1);
   read(0, 0, 0);
+  if (STAG && wave >= NW / 2) {
+    // the late half: ks 0-1 of tile 0 now, then two k-steps behind
+    read(0, 1, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(0);
+    __builtin_amdgcn_sched_barrier(0);
+    read(0, 2, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(1);
+    __builtin_amdgcn_sched_barrier(0);
+    for (int kt = 0; kt < ktiles; ++kt) {
+      read(kt, 3, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(0);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(1);
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + 1 < ktiles) {
+        wait_tile(kt + 2 < ktiles ? 1 : 0);
+        __builtin_amdgcn_s_barrier();
+        if (kt + STAGES < ktiles) issue(kt + STAGES);
+        read(kt + 1, 0, 0);
+        read(kt + 1, 1, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(0);
+        __builtin_amdgcn_sched_barrier(0);
+        read(kt + 1, 2, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else
   for (int kt = 0; kt < ktiles; ++kt) {
     // k-steps 0..2: the next step's reads, then this step's MFMAs
     read(kt, 1, 1);
@@ -1150,6 +1190,8 @@ int launch_i8_gemm(hipStream_t s, const I8Layer &L, const int8_t *a, int lda, in
       // 16: 15's tiles with the loop software-pipelined (gemm_i8_pipe_kernel)
       case 16: go(gemm_i8_pipe_kernel<256, 128, 3, 4, 2>, 256, 128, 512); break;
 #ifdef CATEARS_EXPERIMENTS  // tools/i8_sweep.sh
+      // 17: 16 with waves 4-7 two k-steps behind waves 0-3 (stagger)
+      case 17: go(gemm_i8_pipe_kernel<256, 128, 3, 4, 2, true>, 256, 128, 512); break;
       case 2: go(gemm_i8_glds_kernel<128, 128, 3>, 128, 128); break;
       case 3: go(gemm_i8_glds_kernel<128, 128, 4>, 128, 128); break;
       case 4: go(gemm_i8_glds_kernel<128, 64, 4>, 128, 64); break;

@@ -3,8 +3,10 @@ selected by the experiments library's CATEARS_* switches (read once per
 process: one child process each, on libcatears_hip_exp.so -- the product
 library compiles the defaults in and reads no environment).  Every variant accumulates each output element over the same
 K-tiles in the same order with the same six products per tile,
-so the tile shape (128 x 128, variant 40) and the warp-specialised producer /
-MFMA-wave split (200) must not change any bit of TDNN-S's output.  A value
+so the tile shape (128 x 128, variant 40; 256 x 128, the rounds 3-5 default
+300; the product's 512 x 128 of 8 waves), the warp-specialised producer /
+MFMA-wave split (200) and the one-wave-per-SIMD forms (500-507) must not
+change any bit of TDNN-S's output.  A value
 the product build does not carry (measurement variants, the DIAG ablations)
 fails loudly with CE_GPU_EINVAL instead of running something else.  The
 product library's own choices (wide tiles) run in-process on it."""
@@ -53,7 +55,9 @@ def test_x6_variants_bit_identical(tmp_path, s_config, exp_lib):
     assert np.array_equal(_run(0, s_config, tmp_path / "e0.npy", lib=exp_lib), base), \
         "the experiments library's default differs from the product library"
     assert base.ndim == 2 and base.shape[0] > 0
-    for v in (40, 200):
+    # 300: the rounds 3-5 default (256 x 128 tiles of gemm_bf16x6d_kernel);
+    # 500-507: the one-wave-per-SIMD forms of gemm_bf16x6w_kernel
+    for v in (40, 200, 300, 500, 501, 502, 503, 505, 507):
         got = _run(v, s_config, tmp_path / f"v{v}.npy", lib=exp_lib)
         assert np.array_equal(got, base), f"variant {v} differs from the default"
     # the first layer's splice + row gather in the default kernel's loader
