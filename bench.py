@@ -245,9 +245,10 @@ def cpu_baseline(conf, n_utts, seconds, threads, min_wall):
 ROOFLINE_KERNEL = "gemm_f32_glds_kernel<catears::Cfg<128, 64, 32, 2, 2>, 2, false>"
 # split-plane hidden layers (split output), the default variants
 SPLIT_ROOFLINE_KERNEL = {
-    # CATEARS_X6_VARIANT 0 = 300; every instantiation (the first layer
-    # gathered in the loader on 128 x 128 tiles, layers 2-7 on 256 x 128)
-    "bf16x6": "gemm_bf16x6d_kernel<catears::X6Cfg<*",
+    # the default: the first layer gathered in the loader on 128 x 128 tiles
+    # (gemm_bf16x6d_kernel), layers 2-7 on 512 x 128 (gemm_bf16x6w_kernel);
+    # every launch of both templates
+    "bf16x6": "gemm_bf16x6*",
     "bf16x6_160": "gemm_bf16x6f_kernel<catears::X6Cfg<128, 256, 2, 4, 2>, 8, 0, false>",
     "bf16x6p": "gemm_bf16x6q_kernel<catears::X6Cfg<128, 128, 4, 2, 3>, true, 0>",
     "f16x3": "gemm_f16x3_kernel<catears::X3Cfg<128, 128, 2, 4, 2, 64>, true>",
@@ -262,7 +263,7 @@ SPLIT_DTYPE = {
              "significant bits, 3 MFMA products in 2 fp32 accumulators; error vs oracle at the fp32-MFMA "
              "path's level, tests/test_gpu_parity.py)",
 }
-I8_ROOFLINE_KERNEL = "gemm_i8_pipe_kernel<256, 128, 3, 4, 2>"  # CATEARS_I8_GEMM default 16 (nnet_i8.hip)
+I8_ROOFLINE_KERNEL = "gemm_i8_pipe_kernel<256, 128, 3, 4, 2*"  # CATEARS_I8_GEMM default 16 (nnet_i8.hip), any STAG
 
 
 def gemm_algorithmic_bytes(rows, layers=((3072, 1024),) * 4 + ((1024, 1024), (1024, 3456))):

@@ -1471,13 +1471,32 @@ int launch_d(hipStream_t s, X6Args p) {
   return CE_GPU_OK;
 }
 
+// 512 x 128 tiles (the default kernel) only for layers of at least this many
+constexpr int kX6WideMinTiles = 48;
+
 // the one-wave-per-SIMD kernel; false when the fragment image does not cover
 // the last unit tile (the image pads units to a multiple of 256)
+// The XCD tile groups of the 512-unit tiles (tile_order.h), by the layer's
+// column tiles.  A 1024-unit layer (2 column tiles, 64 tiles): groups of 1
+// put 8 row panels x 1 weight panel on each XCD (each row panel fetched into
+// 2 XCDs' L2s, each weight panel into 4 -- the a . w = 8 minimum of DESIGN.md
+// §8 r5): PMC 200 MB per hidden-layer launch against 223 MB with groups of 2
+// (the whole width, a = 1, w = 8), C3 +1.1 % at the driver's flags
+// (profiles/r06h_group_abc.txt).  The 3456-unit output layer (7 column
+// tiles) keeps groups of 2: 214 MB against 243 MB.  CATEARS_X6W_GROUP
+// (experiments library) forces one value.
+int x6w_group(int tiles_n) {
+  static int v = CE_KNOB("CATEARS_X6W_GROUP", 0);
+  return v > 0 ? v : (tiles_n <= 2 ? 1 : 2);
+}
+
 template <class C, bool SG = false, int RING = 4>
-bool launch_w(hipStream_t s, X6Args p) {
+bool launch_w(hipStream_t s, X6Args p, int min_tiles = 0) {
   p.tiles_n = (p.n + C::BW - 1) / C::BW;
   p.tiles_m = (p.m + C::BF - 1) / C::BF;
   if ((p.n + 255) / 256 * 256 < p.tiles_n * C::BW) return false;
+  if (p.tiles_n * p.tiles_m < min_tiles) return false;
+  p.group = x6w_group(p.tiles_n);
   hipLaunchKernelGGL((gemm_bf16x6w_kernel<C, SG, RING>), dim3(p.tiles_m * p.tiles_n), dim3(C::NT), 0, s, p);
   return true;
 }
@@ -1625,7 +1644,11 @@ int launch_gemm_bf16x6(hipStream_t s, const X6Gemm &a) {
           // for 128 units -- half the activation path and LDS reads per
           // product of 256 x 128; falls back when the
           // fragment image (units padded to 256) does not cover the last tile
-          if (x6_variant() == 0 && !first && launch_w<W6Cfg<512, 128, 4, 2>, true>(s, p)) {
+          // -- when the layer has enough of them to spread over the chip
+          // beside the other streams' batches (a 4096-row batch's hidden
+          // layer: 64); a small block (a 70-row streaming chunk: 2 tiles)
+          // keeps the 256 x 128 tiles
+          if (x6_variant() == 0 && !first && launch_w<W6Cfg<512, 128, 4, 2>, true>(s, p, kX6WideMinTiles)) {
             CE_HIP(hipGetLastError());
             return CE_GPU_OK;
           }

@@ -127,7 +127,10 @@ def check(path, by_tmpl, win_us):
         raise SystemExit(f"--check: no bench line with a roofline in {path}")
     rf = line["roofline"]
     tmpl = rf["kernel"].split("<")[0].split(" ")[0]
-    iv = by_tmpl.get(tmpl)
+    if tmpl.endswith("*"):  # every template with this prefix (e.g. gemm_bf16x6*: the d and w kernels)
+        iv = [x for k, v in by_tmpl.items() if k.startswith(tmpl[:-1]) for x in v]
+    else:
+        iv = by_tmpl.get(tmpl)
     print()
     print(f"check against {path}:")
     if not iv:
