@@ -31,12 +31,14 @@ sys.path.insert(0, ROOT)
 
 
 def default_back_streams(workload):
-    """nnet streams per process when --back-streams is not given: 8 for C3,
-    whose default GEMM (512 x 128 tiles, 64 blocks per hidden layer) needs
-    more batches in flight to fill the chip (profiles/r06f_driver_abba.txt:
-    8 streams + the last batch on wide tiles +2.5 % at the driver's flags
-    over the 256 x 128 kernel on 3); 3 for the other workloads."""
-    return 8 if workload == "c3" else 3
+    """nnet streams per process when --back-streams is not given: 8 for C3
+    and C4, whose default GEMM (512 x 128 tiles, 64 blocks per hidden layer)
+    needs more batches in flight to fill the chip (profiles/r06h_group_abc.txt:
+    C3 with 8 streams + the last batch on wide tiles +2.3 % at the driver's
+    flags over the 256 x 128 kernel on 3; profiles/r06i_streams.txt: C4
+    6.65 M against 6.20 M on 3); 3 for C5, whose int8 GEMM runs 256 blocks
+    per layer (4-8 streams: 17-19 M against 23 M)."""
+    return 8 if workload in ("c3", "c4") else 3
 
 
 def _early_arg(argv, name, default):
