@@ -10,7 +10,7 @@ tail -32 gpurun_out/${T}_round.log
 cd "$R" || exit 1
 timeout -k 10 200 python tools/latency.py 200 > gpurun_out/$T/latency.txt 2>&1 || exit 1
 grep "rows    70" gpurun_out/$T/latency.txt
-for i in 1 2; do
+for i in 1 2 3; do
   timeout -k 10 200 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/$T/driver_$i.json 2>/dev/null || exit 1
   cut -c1-170 gpurun_out/$T/driver_$i.json
 done
