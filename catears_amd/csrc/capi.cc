@@ -468,7 +468,7 @@ extern "C" {
 
 const char *ce_gpu_last_error(void) { return last_error(); }
 
-const char *ce_gpu_version(void) { return "catears-mi355x 0.4 (gfx950)"; }
+const char *ce_gpu_version(void) { return "catears-mi355x 0.5 (gfx950)"; }
 
 int ce_gpu_ctx_create(int device, void *stream, ce_gpu_ctx **out) {
   if (!out) return fail(CE_GPU_EINVAL, "out is NULL");
