@@ -238,6 +238,106 @@ __device__ __forceinline__ void quantize_row(const float *__restrict__ x, int ld
   if (lane == 0) rowsum[r] = s;
 }
 
+// The vector path of quantize_row for RPW rows per wave (plain mode: one
+// segment, width and ldx multiples of 4, no row map): every row's loads are
+// issued before any is converted, and the reciprocal product's rare fallback
+// (a non-finite quotient, qbyte) is one wave-level branch per row instead of
+// one per element: the quotients are formed for the whole row, and only if
+// some lane holds a non-finite one are those recomputed by division.  The
+// same arithmetic per element as qbyte: the same bytes and row sums.
+template <int RPW>
+__device__ __forceinline__ void quantize_rows_fast(const float *__restrict__ x, int ldx, int rows, int width,
+                                                   float scale, float zp, int8_t *__restrict__ q, int ldq,
+                                                   int32_t *__restrict__ rowsum, int r0, int lane) {
+  float rs = 1.0f / scale;
+  const bool rs_ok = !(__builtin_isinf(rs) || __builtin_isnan(rs));
+  int32_t rsum[RPW];
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) rsum[i] = 0;
+  for (int c0 = 0; c0 < width; c0 += 1024) {
+    float4 v[RPW][4];
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      const float *xr = x + (int64_t)min(r0 + i, rows - 1) * ldx;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        v[i][j] = *reinterpret_cast<const float4 *>(xr + min(c0 + 4 * lane + 256 * j, width - 4));
+    }
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      if (r0 + i >= rows) break;
+      float qv[16];
+      bool bad = !rs_ok;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float e[4] = {v[i][j].x, v[i][j].y, v[i][j].z, v[i][j].w};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const float q0 = e[t] * rs;
+          const float qq = __builtin_fmaf(__builtin_fmaf(-scale, q0, e[t]), rs, q0);
+          bad |= __builtin_isinf(qq) || __builtin_isnan(qq);
+          qv[4 * j + t] = qq;
+        }
+      }
+      if (__builtin_amdgcn_ballot_w64(bad)) {  // rare: the division, exactly as qbyte
+        if (bad) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float e[4] = {v[i][j].x, v[i][j].y, v[i][j].z, v[i][j].w};
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+              if (!rs_ok || __builtin_isinf(qv[4 * j + t]) || __builtin_isnan(qv[4 * j + t])) qv[4 * j + t] = e[t] / scale;
+          }
+        }
+      }
+      int8_t *os = q + (int64_t)(r0 + i) * ldq;
+      int32_t &sum = rsum[i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = c0 + 4 * lane + 256 * j;
+        if (c >= width) break;
+        int b[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          float w = qv[4 * j + t] + zp;
+          w = (255.0f < w) ? 255.0f : w;
+          w = (0.0f < w) ? w : 0.0f;
+          b[t] = (int)(uint8_t)roundf(w) - 128;
+          sum += b[t];
+        }
+        const uint32_t packed = (uint32_t)(uint8_t)b[0] | ((uint32_t)(uint8_t)b[1] << 8) |
+                                ((uint32_t)(uint8_t)b[2] << 16) | ((uint32_t)(uint8_t)b[3] << 24);
+        *reinterpret_cast<uint32_t *>(os + c) = packed;
+      }
+    }
+  }
+  // the row sums (exact int32: any order)
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    int32_t sum = rsum[i];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
+    if (lane == 0 && r0 + i < rows) rowsum[r0 + i] = sum;
+  }
+  // zero padding past the row (ldq > width)
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    if (r0 + i >= rows) break;
+    int8_t *o = q + (int64_t)(r0 + i) * ldq;
+    for (int c = width + lane; c < ldq; c += 64) o[c] = 0;
+  }
+}
+
+template <int RPW>
+__global__ __launch_bounds__(256) void quantize_fast_kernel(const float *__restrict__ x, int ldx, int rows, int width,
+                                                            const QP *__restrict__ params, int8_t *__restrict__ q,
+                                                            int ldq, int32_t *__restrict__ rowsum) {
+  const QP p = *params;
+  const int r0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW, lane = threadIdx.x & 63;
+  if (r0 >= rows) return;
+  quantize_rows_fast<RPW>(x, ldx, rows, width, p.scale, (float)p.zp, q, ldq, rowsum, r0, lane);
+}
+
 __global__ __launch_bounds__(256) void quantize_kernel(const float *__restrict__ x, int ldx, int rows, int width,
                                                        const int *__restrict__ row_map, int nseg,
                                                        SpliceOffsets so, const QP *__restrict__ params,
@@ -1121,7 +1221,22 @@ int launch_i8_quantize(hipStream_t s, const float *x, int ldx, int rows, int wid
                        const int *offs, const void *params, int8_t *q, int ldq, int32_t *rowsum) {
   SpliceOffsets so = {};
   for (int i = 0; i < nseg; ++i) so.off[i] = offs[i];
-  if (rows > 0)
+  // Plain-mode layers (every layer after the first) go through
+  // quantize_fast_kernel: one wave-level fallback branch per row instead of
+  // one per element, same bytes and row sums; C5 +3.0 % (24.29 vs 23.58 M
+  // frames/s, A B C C B A x2 on one box, same checksum,
+  // profiles/r06k_c5_quantize.txt).  CATEARS_I8_QFAST (experiments
+  // library): 0 = quantize_kernel, 2 = two rows per wave (+2.1 %).
+  static const int qfast = CE_KNOB("CATEARS_I8_QFAST", 1);
+  const bool plain = nseg == 1 && !row_map && so.off[0] == 0 && width % 4 == 0 && ldx % 4 == 0 && ldq % 4 == 0 &&
+                     (reinterpret_cast<uintptr_t>(q) & 3) == 0;
+  if (rows > 0 && plain && qfast == 1) {
+    hipLaunchKernelGGL(quantize_fast_kernel<1>, dim3((rows + 3) / 4), dim3(256), 0, s, x, ldx, rows, width,
+                       static_cast<const QP *>(params), q, ldq, rowsum);
+  } else if (rows > 0 && plain && qfast == 2) {
+    hipLaunchKernelGGL(quantize_fast_kernel<2>, dim3((rows + 7) / 8), dim3(256), 0, s, x, ldx, rows, width,
+                       static_cast<const QP *>(params), q, ldq, rowsum);
+  } else if (rows > 0)
     hipLaunchKernelGGL(quantize_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, ldx, rows, width, row_map, nseg,
                        so, static_cast<const QP *>(params), q, ldq, rowsum);
   CE_HIP(hipGetLastError());
