@@ -136,3 +136,30 @@ def test_int8_c5_full_batch(torch, G, ctx, oracle):
     got_ls = G.nnet_propagate(ctx, m_full, dev(torch, x)).cpu().numpy()
     want_ls = oracle.layer_forward({"kind": "log_softmax"}, want)
     assert np.max(np.abs(got_ls - want_ls)) <= LOGLIK_TOL
+
+
+@pytest.mark.parametrize("case", ["dead_layer", "wide_range"])
+def test_int8_quantize_edge_ranges(torch, G, ctx, oracle, case):
+    """Hidden-layer Quantize passes (quantize_fast_kernel) at the edges of the
+    parameter math.  dead_layer: a Linear whose ReLU output is all zero, so
+    the next layer's range is [0, FLT_MIN] (max starts at FLT_MIN,
+    matrix.cc:332) and its scale FLT_MIN / 255 is a denormal: the corrected
+    reciprocal overflows and every element takes the division fallback.
+    wide_range: a Linear scaled by 2^90, outputs near 1e27.  Bit for bit
+    against the oracle either way."""
+    from catears_amd import formats
+    layers, left, right, _ = _tdnn(64, 96, final_logsm=False)
+    lin = [i for i, L in enumerate(layers) if L["kind"] == "linear"]
+    i = lin[1]
+    if case == "dead_layer":
+        layers[i] = dict(layers[i], W=np.zeros_like(layers[i]["W"]), b=np.full_like(layers[i]["b"], -1.0))
+        bn = next(j for j in range(i, len(layers)) if layers[j]["kind"] == "batchnorm")
+        layers[bn] = dict(layers[bn], offset=np.zeros_like(layers[bn]["offset"]))
+    else:
+        layers[i] = dict(layers[i], W=(layers[i]["W"] * np.float32(2.0 ** 90)).astype(np.float32))
+    model = G.Model(ctx, image=formats.nnet_bytes(layers, left, right)).quantize(ctx)
+    x = np.random.default_rng(5).normal(9.0, 3.0, size=(700, 40)).astype(np.float32)
+    got = G.nnet_propagate(ctx, model, dev(torch, x)).cpu().numpy()
+    want = oracle.nnet_propagate_int8(layers, x)
+    assert got.shape == want.shape
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
