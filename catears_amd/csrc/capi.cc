@@ -407,6 +407,13 @@ static int ensure_scratch(ce_gpu_ctx *ctx, size_t bytes) {
 
 // the latency GEMM's slice partials (one window of rows)
 static int ensure_lat_part(ce_gpu_ctx *ctx, size_t floats) {
+#ifdef CATEARS_EXPERIMENTS
+  // the split-K fix-up's tickets (CATEARS_LAT_FIXUP, measured slower:
+  // DESIGN.md §8 round 6), zeroed once: every fix-up launch leaves them zero
+  if (!ctx->lat_tickets.ptr) {
+    CE_TRY(ctx->lat_tickets.upload(std::vector<unsigned>(kX6LatTickets, 0u).data(), kX6LatTickets * sizeof(unsigned)));
+  }
+#endif
   if (ctx->lat_part.bytes >= floats * sizeof(float)) return CE_GPU_OK;
   CE_HIP(hipStreamSynchronize(ctx->stream));
   return ctx->lat_part.alloc(floats * sizeof(float));
@@ -1080,7 +1087,7 @@ static int run_steps_x6f(ce_gpu_ctx *ctx, const ce_gpu_model *m, const float *x,
         const size_t pf = x6_lat_part_floats(a.m, a.n, x6_lat_slices(a.kpad, a.n));
         CE_TRY(ensure_lat_part(ctx, pf));
         if (last && lat_fused_final()) a.tail = tail;  // the reduce may run inside the finalize
-        CE_TRY(launch_gemm_bf16x6_lat(ctx->stream, a, ctx->lat_part.as<float>(), pf));
+        CE_TRY(launch_gemm_bf16x6_lat(ctx->stream, a, ctx->lat_part.as<float>(), pf, ctx->lat_tickets.as<unsigned>()));
       } else if (!(diag_skip() & (i == 0 ? 1 : last ? 16 : 32))) {
         CE_TRY(launch_gemm_bf16x6(ctx->stream, a));
       }

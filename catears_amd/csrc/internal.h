@@ -336,6 +336,7 @@ struct ce_gpu_ctx {
   catears::DevBuf blk_maps;    // ce_gpu_nnet_propagate_blocks: row_dst + row_edge
   catears::DevBuf overflow;    // int: an f16x3 split left the fp16 range (ce_gpu_ctx_overflow)
   catears::DevBuf lat_part;    // latency GEMM: slice partials (grown on demand)
+  catears::DevBuf lat_tickets; // latency GEMM fix-up: kX6LatTickets words, zero between launches
   int latency = 0;             // ce_gpu_ctx_set_latency: split-K GEMMs for small batches
   int wide_tiles = 0;          // ce_gpu_ctx_set_wide_tiles: 128 x 128 bf16x6 tiles (all CUs per launch)
   int fbank_mode = 0;          // ce_gpu_ctx_set_fbank: CE_GPU_FBANK_EXACT / _FAST
@@ -473,7 +474,10 @@ constexpr int kX6DirUnits = 256;  // gemm_bf16x6d_kernel's unit tile
 constexpr int kX6LatWindow = 1024;
 int x6_lat_slices(int kpad, int n);
 size_t x6_lat_part_floats(int rows, int n, int slices);
-int launch_gemm_bf16x6_lat(hipStream_t s, const X6Gemm &a, float *part, size_t part_floats);
+// tickets: kX6LatTickets zeroed words for the split-K fix-up (may be null)
+constexpr int kX6LatTickets = 1024;
+int launch_gemm_bf16x6_lat(hipStream_t s, const X6Gemm &a, float *part, size_t part_floats,
+                           unsigned *tickets = nullptr);
 // The last layer's slice reduce fused with the finalize: rows first ..
 // first + rows - 1 of a deferred tail summed, + bias, post chain, then
 // (log-softmax) - prior into out (row_dst as launch_finalize) -- the bits of

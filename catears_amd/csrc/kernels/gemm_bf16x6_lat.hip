@@ -44,6 +44,7 @@ constexpr int kLatNW = 4;              // waves per block, 16 units each
 constexpr int kLatBW = 16 * kLatNW;    // units per block
 constexpr int kLatMaxKt = 8;           // K-tiles (of 32) per slice: all its weights in registers
 constexpr int kLatTarget = 256;        // blocks per row tile the slice rule aims at
+constexpr int kLatTickets = kX6LatTickets;  // output tiles the fix-up can take
 
 struct LatArgs {
   const float *xf;
@@ -56,6 +57,15 @@ struct LatArgs {
   int slices, per;  // S, K-tiles per slice
   int tiles_n, row0, rows;  // this window: rows row0 .. row0 + rows - 1
   int row_tiles, rtb;       // row tiles in the window, row tiles per block
+  // FIX (lat_gemm_kernel): the tile's last slice block to finish does the
+  // reduce + bias + post chain (lat_fix_tail) -- one ticket per output tile
+  // (zeroed once at allocation, reset by that block)
+  unsigned *tickets;
+  const float *bias, *bn_scale, *bn_offset;
+  float *y;
+  int ldy;
+  int post[4];
+  int npost, post_mode;
 };
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
@@ -82,8 +92,69 @@ __device__ __forceinline__ Planes2 split3_pair(float a, float b) {
 // tile is straight-line code (a loop would make the compiler drain the weight
 // loads before the activation loads are issued, at the loop header).
 // KT: K-tiles per slice the block is sized for (>= the slice's per).
-template <int TF, int KT, bool MULTI, int DIAG = 0>
+// The split-K fix-up (FIX, one row tile per block): the partial tiles are
+// stored at agent scope (written through the XCD's L2 to the device's
+// coherence point), each block waits for its stores to be acknowledged and
+// takes its output tile's ticket, and the block that draws the last ticket
+// reads the S partials back at agent scope, sums them in slice order
+// (lat_slice_sum's order) and applies the bias and the post chain -- the
+// reduce launch's arithmetic without its launch.  No block waits on another.
+template <int TF>
+__device__ __forceinline__ void lat_fix_tail(const LatArgs &p, int f0, int n0, int t, int *flag) {
+  typedef unsigned long long u64;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned k = __hip_atomic_fetch_add(p.tickets + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[0] = k == (unsigned)p.slices - 1;
+  }
+  __syncthreads();
+  if (!flag[0]) return;
+  constexpr int BF = 16 * TF, CH = BF * (kLatBW / 4);  // float4 chunks of the tile
+  constexpr int NT = 64 * kLatNW, PER = (CH + NT - 1) / NT;
+  const size_t stride = (size_t)p.rows * p.n;
+  with_post_mode(p.post_mode, [&](auto M) {
+    constexpr int MODE = decltype(M)::value;
+#pragma unroll
+    for (int c = 0; c < PER; ++c) {
+      const int q = threadIdx.x + c * NT;
+      const int f = f0 + q / (kLatBW / 4), n = n0 + 4 * (q % (kLatBW / 4));
+      if (q >= CH || f >= p.row0 + p.rows || f >= p.m || n >= p.n) continue;
+      const u64 *src = reinterpret_cast<const u64 *>(p.part + (size_t)(f - p.row0) * p.n + n);
+      float4 sum = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      for (int s0 = 0; s0 < p.slices; s0 += 16) {
+        u64 v[16][2];
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (s0 + u < p.slices) {
+            const u64 *a = src + (size_t)(s0 + u) * stride / 2;
+            v[u][0] = __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v[u][1] = __hip_atomic_load(a + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (s0 + u < p.slices) {
+            const float4 x = make_float4(__uint_as_float((uint32_t)v[u][0]), __uint_as_float((uint32_t)(v[u][0] >> 32)),
+                                         __uint_as_float((uint32_t)v[u][1]), __uint_as_float((uint32_t)(v[u][1] >> 32)));
+            sum = s0 + u == 0 ? x : make_float4(sum.x + x.x, sum.y + x.y, sum.z + x.z, sum.w + x.w);
+          }
+      }
+      const f32x4 sm = f32x4{sum.x, sum.y, sum.z, sum.w};
+      const f32x4 bias = p.bias ? *reinterpret_cast<const f32x4 *>(p.bias + n) : f32x4{-0.0f, -0.0f, -0.0f, -0.0f};
+      const f32x4 sc = p.bn_scale ? *reinterpret_cast<const f32x4 *>(p.bn_scale + n) : f32x4{1.0f, 1.0f, 1.0f, 1.0f};
+      const f32x4 of = p.bn_offset ? *reinterpret_cast<const f32x4 *>(p.bn_offset + n) : f32x4{-0.0f, -0.0f, -0.0f, -0.0f};
+      f32x4 y;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) y[e] = apply_post<MODE>(sm[e] + bias[e], sc[e], of[e], p.post, p.npost);
+      *reinterpret_cast<f32x4 *>(p.y + (int64_t)f * p.ldy + n) = y;
+    }
+  });
+  if (threadIdx.x == 0) __hip_atomic_store(p.tickets + t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int TF, int KT, bool MULTI, int DIAG = 0, bool FIX = false>
 __global__ __launch_bounds__(64 * kLatNW, MULTI && TF == 4 && KT <= 6 ? 2 : 1) void lat_gemm_kernel(LatArgs p) {
+  static_assert(!(FIX && MULTI), "the fix-up takes one row tile per block");
 #ifndef CATEARS_DIAG
   static_assert(DIAG == 0, "diagnostic schedules are CATEARS_DIAG builds only");
 #endif
@@ -235,9 +306,19 @@ __global__ __launch_bounds__(64 * kLatNW, MULTI && TF == 4 && KT <= 6 ? 2 : 1) v
     for (int j = 0; j < TF; ++j) {
       const int f = f0 + j * 16 + (lane & 15);
       if (f >= p.row0 + p.rows || f >= p.m) continue;
-      *reinterpret_cast<f32x4 *>(p.part + ((size_t)s * p.rows + (f - p.row0)) * p.n + n) = acc[j];
+      float *dst = p.part + ((size_t)s * p.rows + (f - p.row0)) * p.n + n;
+      if constexpr (FIX) {
+        typedef unsigned long long u64;
+        const u64 lo = (u64)__float_as_uint(acc[j][0]) | (u64)__float_as_uint(acc[j][1]) << 32;
+        const u64 hi = (u64)__float_as_uint(acc[j][2]) | (u64)__float_as_uint(acc[j][3]) << 32;
+        __hip_atomic_store(reinterpret_cast<u64 *>(dst), lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(reinterpret_cast<u64 *>(dst) + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        *reinterpret_cast<f32x4 *>(dst) = acc[j];
+      }
     }
   }
+  if constexpr (FIX) lat_fix_tail<TF>(p, f0, n0, t, reinterpret_cast<int *>(smem));
   if constexpr (!MULTI) break;
   }  // row tiles
 }
@@ -351,15 +432,22 @@ void launch_lat_gemm_kt(hipStream_t s, const LatArgs &p, dim3 grid, dim3 block) 
 #endif
   if (p.rtb > 1)
     hipLaunchKernelGGL((lat_gemm_kernel<TF, KT, true>), grid, block, 0, s, p);
+#ifdef CATEARS_EXPERIMENTS
+  else if (p.tickets)
+    hipLaunchKernelGGL((lat_gemm_kernel<TF, KT, false, 0, true>), grid, block, 0, s, p);
+#endif
   else
     hipLaunchKernelGGL((lat_gemm_kernel<TF, KT, false>), grid, block, 0, s, p);
 }
 
+// Returns whether the GEMM also did the reduce (the fix-up: p.tickets set,
+// one row tile per block, few enough output tiles for the ticket array).
 template <int TF>
-void launch_lat_gemm(hipStream_t s, LatArgs p) {
+bool launch_lat_gemm(hipStream_t s, LatArgs p) {
   p.row_tiles = (p.rows + 16 * TF - 1) / (16 * TF);
   p.rtb = lat_rtb(p.row_tiles, p.tiles_n * p.slices);
   const int groups = (p.row_tiles + p.rtb - 1) / p.rtb;
+  if (p.rtb > 1 || groups * p.tiles_n > kLatTickets) p.tickets = nullptr;
   const dim3 grid(groups * p.tiles_n * p.slices), block(64 * kLatNW);
   // the block sized for the slice (its weights all in registers)
   if (p.per <= 2)
@@ -370,6 +458,7 @@ void launch_lat_gemm(hipStream_t s, LatArgs p) {
     launch_lat_gemm_kt<TF, 6>(s, p, grid, block);
   else
     launch_lat_gemm_kt<TF, 8>(s, p, grid, block);
+  return p.tickets != nullptr;
 }
 
 }  // namespace
@@ -395,7 +484,7 @@ size_t x6_lat_part_floats(int rows, int n, int slices) {
   return (size_t)std::min(rows, kX6LatWindow) * (size_t)n * (size_t)slices;
 }
 
-int launch_gemm_bf16x6_lat(hipStream_t s, const X6Gemm &a, float *part, size_t part_floats) {
+int launch_gemm_bf16x6_lat(hipStream_t s, const X6Gemm &a, float *part, size_t part_floats, unsigned *tickets) {
   if (a.tail) a.tail->active = false;
   if (a.m <= 0 || a.n <= 0) return CE_GPU_OK;
   // the last layer's reduce inside the finalize when the rows are one window
@@ -440,19 +529,37 @@ int launch_gemm_bf16x6_lat(hipStream_t s, const X6Gemm &a, float *part, size_t p
   for (int i = 0; i < 4; ++i) r.post[i] = a.post[i];
   r.npost = a.npost;
   r.post_mode = post_mode(a.post, a.npost);
+  // the fix-up (experiments library: CATEARS_LAT_FIXUP=1) for layers reduced
+  // here; its tickets are zero between launches
+#ifdef CATEARS_EXPERIMENTS
+  static const int fixup = CE_KNOB("CATEARS_LAT_FIXUP", 0);
+#else
+  const int fixup = 0;
+#endif
+  p.tickets = fixup && reduce ? tickets : nullptr;
+  p.bias = a.bias;
+  p.bn_scale = a.bn_scale;
+  p.bn_offset = a.bn_offset;
+  p.y = a.y32;
+  p.ldy = a.ldy;
+  for (int i = 0; i < 4; ++i) p.post[i] = a.post[i];
+  p.npost = a.npost;
+  p.post_mode = r.post_mode;
   for (int r0 = 0; r0 < a.m; r0 += kX6LatWindow) {
     p.row0 = r.row0 = r0;
     p.rows = r.rows = std::min(kX6LatWindow, a.m - r0);
     if ((size_t)p.rows * a.n * p.slices > part_floats || !part)
       return fail(CE_GPU_EINVAL, "gemm_bf16x6 latency: partial workspace too small");
     // the frame tile fitting the block (results do not depend on it)
+    bool fixed;
     if (p.rows <= 32)
-      launch_lat_gemm<2>(s, p);
+      fixed = launch_lat_gemm<2>(s, p);
     else if (p.rows <= 80)
-      launch_lat_gemm<5>(s, p);
+      fixed = launch_lat_gemm<5>(s, p);
     else
-      launch_lat_gemm<4>(s, p);  // many row tiles: 64-row tiles, two blocks per CU
+      fixed = launch_lat_gemm<4>(s, p);  // many row tiles: 64-row tiles, two blocks per CU
     CE_HIP(hipGetLastError());
+    if (fixed) continue;
     if (!reduce) {
       LatTail &t = *a.tail;
       t.active = true;

@@ -152,6 +152,23 @@ def test_latency_fused_final_reduce_exact(tmp_path, s_config, exp_lib):
     assert np.array_equal(got["1"], got["0"])
 
 
+def test_latency_fixup_reduce_exact(tmp_path, s_config, exp_lib):
+    """The split-K fix-up (the tile's last slice block does the reduce,
+    CATEARS_LAT_FIXUP=1, an experiments-library variant measured slower:
+    profiles/r06o_lat_fixup.txt) gives the bits of the reduce launch."""
+    from conftest import ROOT
+    got = {}
+    for flag in ("1", "0"):
+        env = dict(os.environ, CATEARS_LAT_FIXUP=flag, PYTHONPATH=ROOT, CATEARS_HIP_LIB=exp_lib)
+        path = tmp_path / f"x{flag}.npy"
+        r = subprocess.run([sys.executable, "-c", FUSED_CHILD, s_config, str(path)], env=env, capture_output=True,
+                           text=True, timeout=300, cwd=ROOT)
+        assert r.returncode == 0, r.stderr[-3000:]
+        got[flag] = np.load(path).view(np.uint32)
+    assert got["1"].size > 0
+    assert np.array_equal(got["1"], got["0"])
+
+
 def test_first_layer_reads_stay_inside_the_input(torch, G, lctx, xs_config):
     """The first layer reads the caller's 40-wide rows directly; its K
     padding (5 x 40 = 200 of 224 / 256) loads column 0 of a valid row, never
