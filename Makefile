@@ -56,7 +56,8 @@ $(OBJ)/gemm_bf16x6.o: HIPFLAGS += -fno-slp-vectorize $(X6FLAGS)
 # the exact fbank kernel holds a frame's FFT in 64 registers per lane: the
 # SLP vectorizer's packed f32 pairs cost it ~20 registers of shuffles and
 # pushed it into scratch
-$(OBJ)/fbank.o: HIPFLAGS += -fno-slp-vectorize
+$(OBJ)/fbank.o $(OBJ)/fbank_nocase.o: HIPFLAGS += -fno-slp-vectorize
+$(OBJ)/fbank_nocase.o: $(SRC)/kernels/fbank.hip
 
 # CMVNFLAGS: experiment defines for the CMVN kernel (e.g. -DCMVN_TILE=48)
 $(OBJ)/cmvn.o: HIPFLAGS += $(CMVNFLAGS)

@@ -850,6 +850,11 @@ int ce_gpu_fbank(ce_gpu_ctx *ctx, const ce_gpu_plan *p, const float *d_pcm, floa
   ProfScope prof(ctx, CE_GPU_PROF_FBANK);
   if (diag_skip() & 4) return CE_GPU_OK;
   const FbankTables *t = ctx->d_tables.as<FbankTables>();
+#ifdef CATEARS_EXPERIMENTS
+  // timing only: phase A without its lane-dependent twiddle cases
+  static const int nocase = CE_KNOB("CATEARS_FB_NOCASE", 0);
+  if (nocase && ctx->fbank_mode != CE_GPU_FBANK_FAST) return launch_fbank_nocase(ctx->stream, t, p, d_pcm, d_feats, d_mel);
+#endif
   return ctx->fbank_mode == CE_GPU_FBANK_FAST ? launch_fbank_fma(ctx->stream, t, p, d_pcm, d_feats, d_mel)
                                               : launch_fbank(ctx->stream, t, p, d_pcm, d_feats, d_mel);
 }

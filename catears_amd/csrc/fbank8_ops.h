@@ -203,7 +203,12 @@ CE_HD void node16(float *re, float *im, const float *tw16) {
 // recursion: a node's ops come after its parent's.
 template <class TwFn>
 CE_HD void phase_a(float *re, float *im, int r, TwFn tw) {
+#ifdef FB8_NOCASE  // timing only (kernels/fbank_nocase.hip): every lane takes the table path
+  (void)r;
+  constexpr bool r0 = false, r4 = false;
+#else
   const bool r0 = r == 0;
+#endif
   // length 256 (m/8 = 32: n = r + 8i)
   node_op<0, 8, true, true, false>(re, im, r0, false, tw(0));
   CE_SCHED_FENCE();
@@ -244,7 +249,9 @@ CE_HD void phase_a(float *re, float *im, int r, TwFn tw) {
   node_op<25, 2, true, false, true>(re, im, false, r0, tw(17));
   CE_SCHED_FENCE();
   // length 32 at 0, 64, 96, 128, 192 (m/8 = 4: n = r)
+#ifndef FB8_NOCASE
   const bool r4 = r == 4;
+#endif
   node_op<0, 1, true, true, true>(re, im, r0, r4, tw(18));
   CE_SCHED_FENCE();
   node_op<8, 1, true, true, true>(re, im, r0, r4, tw(19));

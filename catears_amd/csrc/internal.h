@@ -429,6 +429,12 @@ int launch_fbank_s16(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan 
                      float *feats, float *mel);
 // fast mode (ce_gpu_ctx_set_fbank(ctx, CE_GPU_FBANK_FAST))
 // the fast mode: fbank.hip's lane program with FMA contraction (fbank_fma.hip)
+#ifdef CATEARS_EXPERIMENTS  // kernels/fbank_nocase.hip: timing only
+int launch_fbank_nocase(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, const float *pcm, float *feats,
+                        float *mel);
+int launch_fbank_nocase_s16(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, const int16_t *pcm,
+                            float *feats, float *mel);
+#endif
 int launch_fbank_fma(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, const float *pcm, float *feats,
                      float *mel);
 int launch_fbank_fma_s16(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p, const int16_t *pcm,

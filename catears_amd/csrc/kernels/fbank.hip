@@ -37,6 +37,10 @@
 #define FB8_KERNEL fbank_fma_kernel
 #define FB8_LAUNCH launch_fbank_fma
 #define FB8_LAUNCH_S16 launch_fbank_fma_s16
+#elif defined(FB8_NOCASE)
+#define FB8_KERNEL fbank_nocase_kernel
+#define FB8_LAUNCH launch_fbank_nocase
+#define FB8_LAUNCH_S16 launch_fbank_nocase_s16
 #else
 #define FB8_KERNEL fbank_kernel
 #define FB8_LAUNCH launch_fbank
@@ -214,7 +218,7 @@ int FB8_LAUNCH_S16(hipStream_t s, const FbankTables *d_tab, const ce_gpu_plan *p
   return launch_fbank_t(s, d_tab, p, pcm, feats, mel);
 }
 
-#ifndef FB8_FMA
+#if !defined(FB8_FMA) && !defined(FB8_NOCASE)
 int fbank_frames_per_block() { return kFramesPerBlock; }
 #endif
 
