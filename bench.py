@@ -146,10 +146,10 @@ def parse(argv=None):
                          "the library's (bf16x6: three exact bf16 planes, six products, fp32 GEMM)")
     ap.add_argument("--front-streams", type=int, default=1,
                     help="fbank + CMVN streams; consecutive batches alternate between them")
-    ap.add_argument("--wide-tiles", choices=["none", "last", "ends"], default=None,
-                    help="c3: score the last (or the first and the last) batch of each run of steps on 128 x 128 "
-                         "bf16x6 tiles (ce_gpu_ctx_set_wide_tiles: all CUs per launch while the pipeline drains); "
-                         "same bits.  Default: last for c3, none otherwise")
+    ap.add_argument("--wide-tiles", choices=["none", "last", "ends", "last2", "last4", "ends2"], default=None,
+                    help="c3: score the last (or the first and the last, the last 2 / 4, the first 2 and last 2) batch(es) of each run "
+                         "of steps on 128 x 128 bf16x6 tiles (ce_gpu_ctx_set_wide_tiles: all CUs per launch while "
+                         "the pipeline drains); same bits.  Default: last for c3, none otherwise")
     ap.add_argument("--sink-share", type=float, default=None,
                     help="c3 / c4, N > 1: the fraction of steps (c4: of the corpus share) rank 0 scores a batch "
                          "of its own (it also receives and folds every peer's rows).  Default on RCCL: "
@@ -1226,7 +1226,9 @@ def main(argv=None):
             n_scored[0] += 1
         wide = set()
         if todo and args.wide_tiles != "none":
-            wide = {todo[-1]} | ({todo[0]} if args.wide_tiles == "ends" else set())
+            tail = {"last2": 2, "last4": 4, "ends2": 2}.get(args.wide_tiles, 1)
+            head = {"ends": 1, "ends2": 2}.get(args.wide_tiles, 0)
+            wide = set(todo[-tail:]) | set(todo[:head])
         if todo:
             front_stage(todo[0])
         k = 0
@@ -1483,7 +1485,10 @@ def main(argv=None):
             line["verify_ranks"] = verify_ranks
     if args.wide_tiles != "none":
         line["config"]["wide_tiles"] = {"last": "the last batch of each run of steps",
-                                        "ends": "the first and the last batch of each run of steps"}[
+                                        "ends": "the first and the last batch of each run of steps",
+                                        "last2": "the last 2 batches of each run of steps",
+                                        "last4": "the last 4 batches of each run of steps",
+                                        "ends2": "the first 2 and the last 2 batches of each run of steps"}[
             args.wide_tiles] + " on 128 x 128 bf16x6 tiles (ce_gpu_ctx_set_wide_tiles, same bits)"
     if args.rehearse_send and not args.rehearse_peers:
         line["rehearse_send"] = "every batch read once more after it is scored (a sender's local cost); measurement only"
